@@ -1,0 +1,124 @@
+/*
+ * xrs_hip.h -- C ABI of the MI355X-native X-Reed-Solomon codec (libxrs_hip.so).
+ *
+ * This is the drop-in boundary for templexxx/xrs.  The reference has no FFI:
+ * its plugin surface is the Go method set of *XRS (/root/reference/xrs.go).
+ * Each entry point below names the Go symbol it replaces (file:line).  A cgo
+ * shim that keeps the Go method set on top of these calls is in INTEGRATION.md.
+ *
+ * Conventions (mirroring the reference):
+ *  - Shards ("vects") are caller-owned; outputs are written in place; the
+ *    library retains no pointer after a call returns (sync calls) or after
+ *    the stream reaches the call (async calls).
+ *  - Every function returns an int status: 0 = OK, negative = error.
+ *    xrs_strerror() gives the text; xrs_format_error() rebuilds the exact Go
+ *    message (e.g. "vect size not even: 3") from the code and its argument.
+ *  - The codec is immutable after xrs_new() and safe to share across threads.
+ *  - Sync calls take HOST pointers (like Go []byte) and block until done.
+ *  - *_batched calls take DEVICE pointers to many stripes and are async on the
+ *    given stream (a hipStream_t passed as void*; NULL = default stream).
+ *    Stripe s, shard i lives at base + s*stripe_stride + i*shard_stride.
+ *    This is the performance path.
+ *  - No torch/HIP types appear in any signature.
+ */
+#ifndef XRS_HIP_H
+#define XRS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define XRS_OK 0
+#define XRS_ERR_ILLEGAL_PARITY (-1)     /* xrs.go:57  "illegal parity"            */
+#define XRS_ERR_SIZE_NOT_EVEN (-2)      /* xrs.go:133 "vect size not even: %d"    */
+#define XRS_ERR_ILLEGAL_DATA_INDEX (-3) /* xrs.go:149 "illegal data index: %d"    */
+#define XRS_ERR_ILLEGAL_VECTS (-4)      /* reedsolomon [dep]: bad d/p or vect count */
+#define XRS_ERR_TOO_FEW_SURVIVORS (-5)  /* reedsolomon [dep]: len(dpHas) < d      */
+#define XRS_ERR_ILLEGAL_INDEX (-6)      /* reedsolomon [dep]: index out of range  */
+#define XRS_ERR_SINGULAR (-7)           /* reedsolomon [dep]: singular survivors  */
+#define XRS_ERR_HIP (-8)                /* HIP runtime failure                    */
+#define XRS_ERR_INVALID_ARG (-9)        /* NULL pointer / bad layout argument     */
+#define XRS_ERR_NO_DEVICE (-10)         /* no GPU visible                         */
+
+typedef struct xrs_codec xrs_codec;
+
+/* Text for a status code (static storage). */
+const char *xrs_strerror(int code);
+/* Go-identical message for (code, arg): arg is the size for SIZE_NOT_EVEN and
+ * the index for ILLEGAL_DATA_INDEX.  Returns the number of bytes written. */
+int xrs_format_error(int code, long long arg, char *buf, size_t buflen);
+/* Library version string, and the gfx target the kernels were built for. */
+const char *xrs_version(void);
+
+/* ---- codec ----------------------------------------------------------- */
+/* xrs.go:55 New(dataNum, parityNum).  Builds the systematic Cauchy generator
+ * over GF(2^8)/0x11d, the XORSet (xrs.go:77-100) and every per-operation
+ * coefficient plan on the host; binds the codec to the current HIP device. */
+int xrs_new(int data_num, int parity_num, xrs_codec **out);
+void xrs_free(xrs_codec *codec);
+/* x.RS.DataNum / x.RS.ParityNum (xrs.go:147, :254). */
+int xrs_data_num(const xrs_codec *codec);
+int xrs_parity_num(const xrs_codec *codec);
+/* x.RS encode matrix (generator), (d+p) x d bytes, row-major. */
+int xrs_gen_matrix(const xrs_codec *codec, uint8_t *out, size_t cap);
+/* x.XORSet[parity_index] (xrs.go:49): data indexes piggybacked on that
+ * parity's b-half, ascending.  *len = 0 if the key is absent. */
+int xrs_xorset(const xrs_codec *codec, int parity_index, int *data_idx, int cap, int *len);
+/* xrs.go:146 GetNeedVects(needReconst) -> aNeed (a-vector indexes, ascending,
+ * excluding k), bNeed = {DataNum, parity index}. a_need needs room for d ints. */
+int xrs_get_need_vects(const xrs_codec *codec, int k, int *a_need, int *a_len, int b_need[2]);
+
+/* ---- synchronous per-stripe calls (host memory, Go-identical semantics) -- */
+/* xrs.go:103 Encode(vects): n == d+p vects of `size` bytes; parity written. */
+int xrs_encode(const xrs_codec *codec, uint8_t *const *vects, int n, size_t size);
+/* xrs.go:175 ReconstOne(vects, needReconst): rebuilds data vect k from the
+ * GetNeedVects set only (other vects are not read). */
+int xrs_reconst_one(const xrs_codec *codec, uint8_t *const *vects, int n, size_t size, int k);
+/* xrs.go:236 Reconst(vects, dpHas, needReconst), including the reference's
+ * side effects: a-halves of every vect not in dpHas are rebuilt, and the
+ * b-halves of surviving parity > d are left in plain-RS form (xrs.go:265). */
+int xrs_reconst(const xrs_codec *codec, uint8_t *const *vects, int n, size_t size,
+                const int *dp_has, int n_has, const int *need, int n_need);
+/* xrs.go:324 Update(oldData, newData, row, parity): parity = p vects. */
+int xrs_update(const xrs_codec *codec, const uint8_t *old_data, const uint8_t *new_data,
+               size_t size, int row, uint8_t *const *parity, int n_parity);
+/* xrs.go:363 Replace(data, replaceRows, parity). */
+int xrs_replace(const xrs_codec *codec, uint8_t *const *data, const int *rows, int n,
+                size_t size, uint8_t *const *parity, int n_parity);
+
+/* ---- batched, device-resident, async (the performance path) ----------- */
+/* Encode n_stripes stripes in place.  One fused pass: RS + piggyback. */
+int xrs_encode_batched(const xrs_codec *codec, uint8_t *base, size_t size,
+                       size_t shard_stride, size_t stripe_stride, size_t n_stripes,
+                       void *stream);
+/* ReconstOne(k) for every stripe (reads only the GetNeedVects set). */
+int xrs_reconst_one_batched(const xrs_codec *codec, uint8_t *base, size_t size,
+                            size_t shard_stride, size_t stripe_stride, size_t n_stripes,
+                            int k, void *stream);
+/* Reconst(dpHas, need) for every stripe (same survivor pattern). */
+int xrs_reconst_batched(const xrs_codec *codec, uint8_t *base, size_t size,
+                        size_t shard_stride, size_t stripe_stride, size_t n_stripes,
+                        const int *dp_has, int n_has, const int *need, int n_need,
+                        void *stream);
+/* Update(old, new, row, parity) for every stripe: old/new rows at
+ * old_base + s*old_stripe_stride (same for new); parity shard r of stripe s at
+ * parity_base + s*parity_stripe_stride + r*parity_shard_stride. */
+int xrs_update_batched(const xrs_codec *codec, const uint8_t *old_base, size_t old_stripe_stride,
+                       const uint8_t *new_base, size_t new_stripe_stride, size_t size, int row,
+                       uint8_t *parity_base, size_t parity_shard_stride,
+                       size_t parity_stripe_stride, size_t n_stripes, void *stream);
+/* Replace(data, rows, parity) for every stripe: data i of stripe s at
+ * data_base + s*data_stripe_stride + i*data_shard_stride. */
+int xrs_replace_batched(const xrs_codec *codec, const uint8_t *data_base,
+                        size_t data_shard_stride, size_t data_stripe_stride, const int *rows,
+                        int n, size_t size, uint8_t *parity_base, size_t parity_shard_stride,
+                        size_t parity_stripe_stride, size_t n_stripes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XRS_HIP_H */

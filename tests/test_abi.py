@@ -1,0 +1,112 @@
+"""CPU tests of the C ABI (include/xrs_hip.h): the library loads, exports every
+declared symbol, and its host logic (New, XORSet, GetNeedVects, generator,
+error texts) matches the reference.  No kernel is launched here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.xrs_oracle import XRS as PyXRS
+from oracle.xrs_oracle import make_xor_set_old
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "xrs_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(xrs_[a-z0-9_]+)\s*\(", src)))
+
+
+def gpu_present():
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        n = ctypes.c_int(0)
+        return hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0
+    except OSError:
+        return False
+
+
+def test_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    lib = ctypes.CDLL(xrs_amd.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_version_mentions_gfx950():
+    assert b"gfx950" in xrs_amd.lib().xrs_version()
+
+
+def test_new_errors():
+    with pytest.raises(xrs_amd.XRSError, match="^illegal parity$"):
+        xrs_amd.XRS(12, 1)
+    for d, p in [(0, 4), (-1, 2), (255, 2), (12, 0)]:
+        with pytest.raises(xrs_amd.XRSError):
+            xrs_amd.XRS(d, p)
+    xrs_amd.XRS(254, 2)
+    xrs_amd.XRS(1, 255)
+
+
+def test_xor_set_and_need_vects_all_configs():
+    """xrs_test.go:51-80 (makeXORSet == makeXORSetOld) and :124-156
+    (aNeed + k == XORSet[bNeed[1]], New succeeds) for every d+p <= 256,
+    through the product library's host logic."""
+    for d in range(1, 256):
+        for p in range(2, 257 - d):
+            x = xrs_amd.XRS(d, p)
+            assert x.xor_set == make_xor_set_old(d, p), (d, p)
+            if p in (2, 3, 4, 7, 256 - d) or d < 8:
+                xs = x.xor_set
+                for i in range(d):
+                    a, b = x.get_need_vects(i)
+                    assert b[0] == d
+                    assert sorted(a + [i]) == xs[b[1]]
+
+
+def test_generator_matches_oracle():
+    for d, p in [(12, 4), (5, 5), (10, 4), (1, 2), (200, 56)]:
+        g = np.frombuffer(xrs_amd.XRS(d, p).gen_matrix, np.uint8).reshape(d + p, d)
+        assert np.array_equal(g, PyXRS(d, p).gen)
+
+
+def test_need_vects_12p4():
+    x = xrs_amd.XRS(12, 4)
+    assert x.xor_set == {13: [0, 3, 6, 9], 14: [1, 4, 7, 10], 15: [2, 5, 8, 11]}
+    for k in range(12):
+        a, b = x.get_need_vects(k)
+        assert b == [12, 13 + k % 3]
+        assert a == [i for i in range(k % 3, 12, 3) if i != k]
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: -1$"):
+        x.get_need_vects(-1)
+
+
+def test_error_messages_are_go_text():
+    x = xrs_amd.XRS(12, 4)
+    with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 5$"):
+        x.encode([np.zeros(5, np.uint8) for _ in range(16)])
+    with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 7$"):
+        x.reconst_one([np.zeros(7, np.uint8) for _ in range(16)], 0)
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: 12$"):
+        x.reconst_one([np.zeros(8, np.uint8) for _ in range(16)], 12)
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: 13$"):
+        x.update(np.zeros(8, np.uint8), np.zeros(8, np.uint8), 13,
+                 [np.zeros(8, np.uint8) for _ in range(4)])
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: 12$"):
+        x.replace([np.zeros(8, np.uint8)], [12], [np.zeros(8, np.uint8) for _ in range(4)])
+    with pytest.raises(xrs_amd.XRSError, match="^illegal vects$"):
+        x.encode([np.zeros(8, np.uint8) for _ in range(15)])
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
+def test_compute_without_gpu_fails_loudly():
+    x = xrs_amd.XRS(12, 4)
+    with pytest.raises(xrs_amd.XRSError, match="no gpu device"):
+        x.encode([np.zeros(8, np.uint8) for _ in range(16)])
+    with pytest.raises(xrs_amd.XRSError, match="no gpu device"):
+        x.encode_batched(1 << 20, 4096, 4096, 65536, 1)

@@ -1,0 +1,401 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle, the
+committed goldens and the reference's property tests (xrs_test.go), plus
+size-independent round-trip properties at BASELINE.json's full sizes.
+
+All tests run in ONE process on the GPU box (python -m pytest tests -m gpu)."""
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+D, P = 12, 4
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch.device("cuda:0")
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def encoded_host(x, rng, size, d=D, p=P):
+    v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d)]
+    v += [np.zeros(size, np.uint8) for _ in range(p)]
+    x.encode(v)
+    return v
+
+
+# ============================================================ sync (host) API
+def test_kat_5p5(cuda):
+    """xrs_test.go:102-122 through the GPU path."""
+    v = [np.array(a, np.uint8) for a in
+         ([0, 0], [4, 7], [2, 4], [6, 9], [8, 11], [0, 0], [0, 0], [0, 0], [0, 0], [0, 0])]
+    xrs_amd.XRS(5, 5).encode(v)
+    assert [list(map(int, a)) for a in v[5:]] == [[97, 156], [173, 117], [218, 110], [107, 59],
+                                                  [110, 153]]
+
+
+@pytest.mark.parametrize("S", [2, 64, 1026, 4096])
+def test_golden_sync(golden, cuda, S):
+    x = xrs_amd.XRS(D, P)
+    v = [r.copy() for r in golden[f"enc_S{S}_in"]] + [np.zeros(S, np.uint8) for _ in range(P)]
+    x.encode(v)
+    assert np.array_equal(np.stack(v), golden[f"enc_S{S}_out"])
+    enc = golden[f"enc_S{S}_out"]
+    i = 0
+    while f"rc{i}_S{S}_has" in golden:
+        v = [r.copy() for r in golden[f"rc{i}_S{S}_in"]]
+        x.reconst(v, list(golden[f"rc{i}_S{S}_has"]), list(golden[f"rc{i}_S{S}_need"]))
+        assert np.array_equal(np.stack(v), golden[f"rc{i}_S{S}_out"]), i
+        i += 1
+    for row in range(D):
+        par = [r.copy() for r in enc[D:]]
+        x.update(enc[row].copy(), golden[f"up_S{S}_row{row}_new"], row, par)
+        assert np.array_equal(np.stack(par), golden[f"up_S{S}_row{row}_out"]), row
+    for n in (1, 4, 12):
+        for z in ("tozero", "fromzero"):
+            rows = [int(r) for r in golden[f"rp_S{S}_n{n}_{z}_rows"]]
+            par = [r.copy() for r in golden[f"rp_S{S}_n{n}_{z}_in"]]
+            x.replace([enc[r].copy() for r in rows], rows, par)
+            assert np.array_equal(np.stack(par), golden[f"rp_S{S}_n{n}_{z}_out"]), (n, z)
+
+
+@pytest.mark.parametrize("size", [2, 4096, 1 << 20])
+def test_reconst_one_need_set_only(cuda, rng, size):
+    """xrs_test.go:158-227: bytes outside GetNeedVects are zeroed first."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    for lost in range(D):
+        exp = encoded_host(o, rng, size)
+        res = [r.copy() for r in exp]
+        res[lost][:] = 0
+        a_need, b_need = x.get_need_vects(lost)
+        half = size // 2
+        for j in range(D + P):
+            if j not in a_need:
+                res[j][:half] = 0
+        for j in range(D, D + P):
+            if j not in b_need:
+                res[j][half:] = 0
+        x.reconst_one(res, lost)
+        assert np.array_equal(res[lost], exp[lost]), lost
+
+
+def test_reconst_random_vs_oracle(cuda, rng):
+    """xrs_test.go:261-314 testReconst (128 loops, S=1024); every buffer is
+    compared with the oracle, so the side effects match too."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    size = 1024
+    for _ in range(128):
+        exp = encoded_host(o, rng, size)
+        lost = [int(v) for v in rng.permutation(D + P)[: int(rng.integers(0, P + 1))]]
+        need = lost[: int(rng.integers(0, len(lost) + 1))]
+        if len(need) == 1:
+            lost = need
+        has = [i for i in range(D + P) if i not in lost]
+        act = [np.zeros(size, np.uint8) for _ in range(D + P)]
+        for h in has:
+            act[h][:] = exp[h]
+        for n in need:
+            if rng.integers(0, 4) == 0:
+                act[n][:] = exp[n]
+        ref = [a.copy() for a in act]
+        x.reconst(act, has, need)
+        o.reconst(ref, has, need)
+        for n in need:
+            assert np.array_equal(act[n], exp[n])
+        assert all(np.array_equal(a, b) for a, b in zip(act, ref))
+
+
+def test_update_sync(cuda, rng):
+    """xrs_test.go:316-359 testUpdate."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    for row in range(D):
+        act = encoded_host(o, rng, 1024)
+        new = rng.integers(0, 256, size=1024, dtype=np.uint8)
+        x.update(act[row], new, row, act[D:])
+        exp = [a.copy() for a in act]
+        exp[row] = new
+        o.encode(exp)
+        assert all(np.array_equal(act[j], exp[j]) for j in range(D, D + P))
+
+
+@pytest.mark.parametrize("to_zero", [True, False])
+def test_replace_sync(cuda, rng, to_zero):
+    """xrs_test.go:361-421 testReplace (1024 loops each direction)."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    size = 1024
+    for _ in range(1024):
+        n = int(rng.integers(0, D + 1))
+        rows = [int(v) for v in rng.permutation(D)[:n]] or [0]
+        full = encoded_host(o, rng, size)
+        data = [full[r].copy() for r in rows]
+        zeroed = [a.copy() for a in full]
+        for r in rows:
+            zeroed[r][:] = 0
+        o.encode(zeroed)
+        act = [a.copy() for a in (full if to_zero else zeroed)]
+        exp = zeroed if to_zero else full
+        x.replace(data, rows, act[D:])
+        assert all(np.array_equal(act[j], exp[j]) for j in range(D, D + P))
+
+
+@pytest.mark.parametrize("d,p", [(1, 2), (2, 3), (5, 5), (10, 4), (6, 3), (20, 8), (3, 9),
+                                 (30, 6), (100, 10)])
+def test_other_configs_sync(cuda, rng, d, p):
+    """Runtime-shaped kernels, output groups (p > 4) and source chunks (d > 24)."""
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    for size in (2, 34, 4096, 4114):
+        v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d)]
+        v += [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(p)]  # garbage parity
+        ref = [a.copy() for a in v]
+        x.encode(v)
+        o.encode(ref)
+        assert all(np.array_equal(a, b) for a, b in zip(v, ref)), size
+        for k in (0, d - 1):
+            a = [r.copy() for r in v]
+            a[k][:] = 0
+            x.reconst_one(a, k)
+            assert np.array_equal(a[k], v[k])
+        lost = [int(t) for t in rng.permutation(d + p)[:p]]
+        need = lost[: max(2, len(lost) - 1)]
+        has = [i for i in range(d + p) if i not in lost]
+        a1 = [r.copy() for r in v]
+        a2 = [r.copy() for r in v]
+        for t in lost:
+            a1[t][:] = 0x5A
+            a2[t][:] = 0x5A
+        x.reconst(a1, has, need)
+        o.reconst(a2, has, need)
+        assert all(np.array_equal(a, b) for a, b in zip(a1, a2)), size
+        row = int(rng.integers(0, d))
+        new = rng.integers(0, 256, size=size, dtype=np.uint8)
+        p1 = [r.copy() for r in v[d:]]
+        p2 = [r.copy() for r in v[d:]]
+        x.update(v[row], new, row, p1)
+        o.update(v[row], new, row, p2)
+        assert all(np.array_equal(a, b) for a, b in zip(p1, p2))
+        rows = [int(t) for t in rng.permutation(d)[: max(1, d // 2)]]
+        data = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in rows]
+        x.replace(data, rows, p1)
+        o.replace(data, rows, p2)
+        assert all(np.array_equal(a, b) for a, b in zip(p1, p2))
+
+
+def test_errors_on_gpu(cuda):
+    x = xrs_amd.XRS(D, P)
+    with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 9$"):
+        x.encode([np.zeros(9, np.uint8) for _ in range(16)])
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: -1$"):
+        x.reconst([np.zeros(8, np.uint8) for _ in range(16)], list(range(16)), [-1])
+    v = [np.zeros(8, np.uint8) for _ in range(16)]
+    with pytest.raises(xrs_amd.XRSError, match="too few survivors"):
+        x.reconst(v, list(range(11)), [12, 13])
+    x.encode([np.zeros(0, np.uint8) for _ in range(16)])  # empty vects: no-op
+
+
+# ============================================================ batched device API
+def batch(rng, n, size, d=D, p=P):
+    return rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+
+
+def oracle_encode_batch(o, host):
+    h = host.copy()
+    n, _, size = h.shape
+    o.encode_batch(h, size, n)
+    return h
+
+
+@pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 65536])
+def test_encode_batched_vs_oracle(cuda, rng, size):
+    n = max(1, (8 << 20) // (16 * size))
+    host = batch(rng, n, size)
+    t = to_dev(host, cuda)
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    x.encode_batched(t.data_ptr(), size, size, 16 * size, n, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), oracle_encode_batch(o, host))
+
+
+def test_encode_batched_padded_layout(cuda, rng):
+    """Shard and stripe strides larger than the vect (and not 16-aligned)."""
+    size, n = 4096, 37
+    for shard_stride, stripe_stride in [(4096 + 16, 16 * (4096 + 16) + 64), (4099, 16 * 4099 + 5)]:
+        buf = rng.integers(0, 256, size=n * stripe_stride, dtype=np.uint8)
+        t = to_dev(buf, cuda)
+        xrs_amd.XRS(D, P).encode_batched(t.data_ptr(), size, shard_stride, stripe_stride, n,
+                                         stream())
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        o = OracleXRS(D, P)
+        for s in range(n):
+            v = [buf[s * stripe_stride + i * shard_stride:][:size].copy() for i in range(D + P)]
+            o.encode(v)
+            for i in range(D + P):
+                off = s * stripe_stride + i * shard_stride
+                assert np.array_equal(got[off:off + size], v[i]), (s, i)
+        # bytes between shards untouched
+        mask = np.ones(len(buf), bool)
+        for s in range(n):
+            for i in range(D + P):
+                off = s * stripe_stride + i * shard_stride
+                mask[off:off + size] = False
+        assert np.array_equal(got[mask], buf[mask])
+
+
+@pytest.mark.parametrize("size", [4096, 1 << 20])
+def test_reconst_one_batched_all_k(cuda, rng, size):
+    n = 8 if size == 1 << 20 else 256
+    o = OracleXRS(D, P)
+    enc = oracle_encode_batch(o, batch(rng, n, size))
+    x = xrs_amd.XRS(D, P)
+    for k in range(D):
+        a_need, b_need = x.get_need_vects(k)
+        h = enc.copy()
+        half = size // 2
+        # garbage everywhere outside the need set
+        for j in range(D + P):
+            if j not in a_need:
+                h[:, j, :half] = 0xA5
+            if j != k and j < D or j in b_need:
+                continue
+            h[:, j, half:] = 0x3C
+        h[:, k] = 0x77
+        t = to_dev(h, cuda)
+        x.reconst_one_batched(t.data_ptr(), size, size, 16 * size, n, k, stream())
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        assert np.array_equal(got[:, k], enc[:, k]), k
+        others = [j for j in range(D + P) if j != k]
+        assert np.array_equal(got[:, others], h[:, others]), k  # nothing else written
+
+
+def test_reconst_batched_vs_oracle(cuda, rng):
+    size, n = 4096, 64
+    o = OracleXRS(D, P)
+    enc = oracle_encode_batch(o, batch(rng, n, size))
+    x = xrs_amd.XRS(D, P)
+    for _ in range(24):
+        lost = [int(v) for v in rng.permutation(D + P)[: int(rng.integers(0, P + 1))]]
+        need = lost[: int(rng.integers(0, len(lost) + 1))]
+        has = [i for i in range(D + P) if i not in lost]
+        h = enc.copy()
+        for t_ in lost:
+            h[:, t_] = rng.integers(0, 256, size=(n, size), dtype=np.uint8)
+        t = to_dev(h, cuda)
+        x.reconst_batched(t.data_ptr(), size, size, 16 * size, n, has, need, stream())
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        for s in range(n):
+            v = [h[s, i].copy() for i in range(D + P)]
+            o.reconst(v, has, need)
+            assert np.array_equal(got[s], np.stack(v)), (lost, need, s)
+
+
+def test_update_replace_batched_vs_oracle(cuda, rng):
+    size, n = 8 << 20, 4
+    o = OracleXRS(D, P)
+    enc = oracle_encode_batch(o, batch(rng, n, size))
+    x = xrs_amd.XRS(D, P)
+    new = rng.integers(0, 256, size=(n, size), dtype=np.uint8)
+    row = 5
+    t = to_dev(enc, cuda)
+    tn = to_dev(new, cuda)
+    S = 16 * size
+    x.update_batched(t.data_ptr() + row * size, S, tn.data_ptr(), size, size, row,
+                     t.data_ptr() + D * size, size, S, n, stream())
+    torch.cuda.synchronize()
+    got = t.cpu().numpy()
+    for s in range(n):
+        par = [enc[s, D + r].copy() for r in range(P)]
+        o.update(enc[s, row], new[s], row, par)
+        assert np.array_equal(got[s, D:], np.stack(par))
+    # Replace(rows 0..3) from zero: parity of a stripe with rows 0..3 zeroed
+    rows = [0, 1, 2, 3]
+    z = enc.copy()
+    z[:, rows] = 0
+    z = oracle_encode_batch(o, z)
+    t = to_dev(z, cuda)
+    data = to_dev(np.ascontiguousarray(enc[:, rows]), cuda)
+    x.replace_batched(data.data_ptr(), size, 4 * size, rows, size, t.data_ptr() + D * size, size,
+                      S, n, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy()[:, D:], enc[:, D:])
+
+
+# ============================================================ full-size properties
+def _dev_random(n_bytes, dev, seed):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (n_bytes,), dtype=torch.uint8, device=dev, generator=g)
+
+
+@pytest.mark.parametrize("size,n", [(4096, 65536), (1 << 20, 512)])
+def test_full_size_encode_erase_reconst(cuda, size, n):
+    """BASELINE configs 2 and 3 at full size (4 GiB / 8 GiB): encode on the GPU,
+    sample stripes against the oracle, then erase data shard k of EVERY stripe
+    and ReconstOne it back (round trip, bit-exact on all stripes)."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    S = 16 * size
+    t = _dev_random(n * S, cuda, 1234)
+    x.encode_batched(t.data_ptr(), size, size, S, n, stream())
+    torch.cuda.synchronize()
+    v = t.view(n, 16, size)
+    for s in (0, 1, n // 2, n - 1):
+        host = v[s].cpu().numpy().copy()
+        ref = [host[i].copy() for i in range(16)]
+        o.encode(ref)
+        assert np.array_equal(host, np.stack(ref)), s
+    for k in (0, 7, 11):
+        keep = v[:, k].clone()
+        v[:, k].fill_(0)
+        x.reconst_one_batched(t.data_ptr(), size, size, S, n, k, stream())
+        torch.cuda.synchronize()
+        assert torch.equal(v[:, k], keep), k
+    # multi-loss: 2 data + 1 parity lost, rebuild all three
+    lost = [3, 9, 14]
+    keep = v[:, lost].clone()
+    v[:, lost] = 0
+    has = [i for i in range(16) if i not in lost]
+    x.reconst_batched(t.data_ptr(), size, size, S, n, has, lost, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(v[:, lost], keep)
+    del t, v, keep
+    torch.cuda.empty_cache()
+
+
+def test_update_linearity_full_size(cuda):
+    """BASELINE config 4 (8 MiB vects): Update then Update back is the identity,
+    and Update equals re-encode on sampled stripes."""
+    size, n = 8 << 20, 32
+    x = xrs_amd.XRS(D, P)
+    S = 16 * size
+    t = _dev_random(n * S, cuda, 99)
+    x.encode_batched(t.data_ptr(), size, size, S, n, stream())
+    v = t.view(n, 16, size)
+    par0 = v[:, D:].clone()
+    new = _dev_random(n * size, cuda, 7).view(n, size)
+    row = 6
+    x.update_batched(v[:, row].data_ptr(), S, new.data_ptr(), size, size, row,
+                     v[:, D].data_ptr(), size, S, n, stream())
+    par1 = v[:, D:].clone()
+    x.update_batched(new.data_ptr(), size, v[:, row].data_ptr(), S, size, row,
+                     v[:, D].data_ptr(), size, S, n, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(v[:, D:], par0)
+    v[:, row] = new
+    x.encode_batched(t.data_ptr(), size, size, S, n, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(v[:, D:], par1)
+    del t, v, par0, par1, new
+    torch.cuda.empty_cache()

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, a short bench, a rocprofv3 kernel
+# trace.  Every GPU step has its own time limit; a crash/timeout ends the run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  return $rc
+}
+STEPS=${STEPS:-pytest,smoke,bench,prof}
+if [[ $STEPS == *pytest* ]]; then
+  run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider ${PYTEST_ARGS:-}
+  rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
+if [[ $STEPS == *smoke* ]]; then
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+fi
+if [[ $STEPS == *bench* ]]; then
+  run bench 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 8} || exit $?
+fi
+if [[ $STEPS == *prof* ]]; then
+  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+      python bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+fi
+exit 0

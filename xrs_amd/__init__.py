@@ -1,0 +1,229 @@
+"""xrs_amd -- MI355X-native X-Reed-Solomon codec (host mirror of templexxx/xrs).
+
+Python mirror of the Go ``*XRS`` method set (/root/reference/xrs.go) over the
+C ABI of ``libxrs_hip.so`` (include/xrs_hip.h).  Every byte of shard arithmetic
+runs in the gfx950 kernels of that library; this module only marshals
+arguments.  There is no CPU fallback: if the library is missing, importing
+this package raises.
+
+    x = XRS(12, 4)                 # xrs.go:55 New
+    x.encode(vects)                # xrs.go:103 Encode (host buffers, in place)
+    x.reconst(vects, dp_has, need) # xrs.go:236 Reconst
+    x.encode_batched(ptr, size, shard_stride, stripe_stride, n_stripes, stream)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+__all__ = ["XRS", "XRSError", "lib", "LIB_PATH"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
+
+XRS_ERR_SIZE_NOT_EVEN = -2
+XRS_ERR_ILLEGAL_DATA_INDEX = -3
+
+
+class XRSError(Exception):
+    """An error returned by the codec; ``str()`` is the Go message text."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"xrs_amd: {LIB_PATH} is not built (run __graft_entry__.build() or "
+            "make -C xrs_amd/csrc); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    I, Z, P = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+    IP = ctypes.POINTER(ctypes.c_int)
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "xrs_strerror": ([I], ctypes.c_char_p),
+        "xrs_format_error": ([I, ctypes.c_longlong, ctypes.c_char_p, Z], I),
+        "xrs_version": ([], ctypes.c_char_p),
+        "xrs_new": ([I, I, ctypes.POINTER(P)], I),
+        "xrs_free": ([P], None),
+        "xrs_data_num": ([P], I),
+        "xrs_parity_num": ([P], I),
+        "xrs_gen_matrix": ([P, P, Z], I),
+        "xrs_xorset": ([P, I, IP, I, IP], I),
+        "xrs_get_need_vects": ([P, I, IP, IP, IP], I),
+        "xrs_encode": ([P, PP, I, Z], I),
+        "xrs_reconst_one": ([P, PP, I, Z, I], I),
+        "xrs_reconst": ([P, PP, I, Z, IP, I, IP, I], I),
+        "xrs_update": ([P, P, P, Z, I, PP, I], I),
+        "xrs_replace": ([P, PP, IP, I, Z, PP, I], I),
+        "xrs_encode_batched": ([P, P, Z, Z, Z, Z, P], I),
+        "xrs_reconst_one_batched": ([P, P, Z, Z, Z, Z, I, P], I),
+        "xrs_reconst_batched": ([P, P, Z, Z, Z, Z, IP, I, IP, I, P], I),
+        "xrs_update_batched": ([P, P, Z, P, Z, Z, I, P, Z, Z, Z, P], I),
+        "xrs_replace_batched": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z, P], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+def _ptr(buf) -> int:
+    """Address of a writable host buffer (numpy array, bytearray, ctypes array)."""
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    if isinstance(buf, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(buf)).from_buffer(buf))
+    return ctypes.addressof(buf)
+
+
+def _ptrs(vects):
+    a = (ctypes.c_void_p * max(1, len(vects)))()
+    for i, v in enumerate(vects):
+        a[i] = _ptr(v)
+    return a
+
+
+def _ints(xs):
+    a = (ctypes.c_int * max(1, len(xs)))()
+    for i, v in enumerate(xs):
+        a[i] = int(v)
+    return a
+
+
+def _raise(code: int, arg: int = 0):
+    if code == 0:
+        return
+    buf = ctypes.create_string_buffer(128)
+    _lib.xrs_format_error(code, int(arg), buf, len(buf))
+    raise XRSError(code, buf.value.decode())
+
+
+class XRS:
+    """The X-Reed-Solomon codec (mirror of Go ``type XRS``, xrs.go:42-50)."""
+
+    def __init__(self, data_num: int, parity_num: int):
+        h = ctypes.c_void_p()
+        _raise(_lib.xrs_new(int(data_num), int(parity_num), ctypes.byref(h)))
+        self._h = h
+        self.data_num = _lib.xrs_data_num(h)
+        self.parity_num = _lib.xrs_parity_num(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.xrs_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---------------------------------------------------------- codec state
+    @property
+    def gen_matrix(self) -> bytes:
+        n = (self.data_num + self.parity_num) * self.data_num
+        buf = ctypes.create_string_buffer(n)
+        _raise(_lib.xrs_gen_matrix(self._h, buf, n))
+        return buf.raw
+
+    @property
+    def xor_set(self) -> dict:
+        """x.XORSet (xrs.go:49): parity index -> data indexes."""
+        out = {}
+        cap = self.data_num
+        arr = (ctypes.c_int * max(1, cap))()
+        n = ctypes.c_int()
+        for h in range(self.data_num + 1, self.data_num + self.parity_num):
+            _raise(_lib.xrs_xorset(self._h, h, arr, cap, ctypes.byref(n)))
+            if n.value:
+                out[h] = [arr[i] for i in range(n.value)]
+        return out
+
+    def get_need_vects(self, need_reconst: int):
+        """xrs.go:146 GetNeedVects -> (aNeed, bNeed)."""
+        a = (ctypes.c_int * max(1, self.data_num))()
+        n = ctypes.c_int()
+        b = (ctypes.c_int * 2)()
+        _raise(_lib.xrs_get_need_vects(self._h, int(need_reconst), a, ctypes.byref(n), b),
+               need_reconst)
+        return [a[i] for i in range(n.value)], [b[0], b[1]]
+
+    # ------------------------------------------------------- sync (host) API
+    def encode(self, vects) -> None:
+        size = len(vects[0]) if len(vects) else 0
+        _raise(_lib.xrs_encode(self._h, _ptrs(vects), len(vects), size), size)
+
+    def reconst_one(self, vects, need_reconst: int) -> None:
+        size = len(vects[0])
+        rc = _lib.xrs_reconst_one(self._h, _ptrs(vects), len(vects), size, int(need_reconst))
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else need_reconst)
+
+    def reconst(self, vects, dp_has, need_reconst) -> None:
+        size = len(vects[0])
+        rc = _lib.xrs_reconst(self._h, _ptrs(vects), len(vects), size, _ints(dp_has),
+                              len(dp_has), _ints(need_reconst), len(need_reconst))
+        arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
+
+    def update(self, old_data, new_data, row: int, parity) -> None:
+        size = len(old_data)
+        rc = _lib.xrs_update(self._h, _ptr(old_data), _ptr(new_data), size, int(row),
+                             _ptrs(parity), len(parity))
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
+
+    def replace(self, data, replace_rows, parity) -> None:
+        size = len(data[0]) if len(data) else 0
+        rc = _lib.xrs_replace(self._h, _ptrs(data), _ints(replace_rows), len(replace_rows), size,
+                              _ptrs(parity), len(parity))
+        bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
+
+    # ------------------------------------------- batched device-resident API
+    # Pointers are device addresses (int); stream is a hipStream_t as int (0 = null).
+    def encode_batched(self, base: int, size: int, shard_stride: int, stripe_stride: int,
+                       n_stripes: int, stream: int = 0) -> None:
+        _raise(_lib.xrs_encode_batched(self._h, base, size, shard_stride, stripe_stride,
+                                       n_stripes, stream), size)
+
+    def reconst_one_batched(self, base: int, size: int, shard_stride: int, stripe_stride: int,
+                            n_stripes: int, k: int, stream: int = 0) -> None:
+        rc = _lib.xrs_reconst_one_batched(self._h, base, size, shard_stride, stripe_stride,
+                                          n_stripes, int(k), stream)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else k)
+
+    def reconst_batched(self, base: int, size: int, shard_stride: int, stripe_stride: int,
+                        n_stripes: int, dp_has, need_reconst, stream: int = 0) -> None:
+        rc = _lib.xrs_reconst_batched(self._h, base, size, shard_stride, stripe_stride, n_stripes,
+                                      _ints(dp_has), len(dp_has), _ints(need_reconst),
+                                      len(need_reconst), stream)
+        arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
+
+    def update_batched(self, old_base: int, old_stripe_stride: int, new_base: int,
+                       new_stripe_stride: int, size: int, row: int, parity_base: int,
+                       parity_shard_stride: int, parity_stripe_stride: int, n_stripes: int,
+                       stream: int = 0) -> None:
+        rc = _lib.xrs_update_batched(self._h, old_base, old_stripe_stride, new_base,
+                                     new_stripe_stride, size, int(row), parity_base,
+                                     parity_shard_stride, parity_stripe_stride, n_stripes, stream)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
+
+    def replace_batched(self, data_base: int, data_shard_stride: int, data_stripe_stride: int,
+                        replace_rows, size: int, parity_base: int, parity_shard_stride: int,
+                        parity_stripe_stride: int, n_stripes: int, stream: int = 0) -> None:
+        rc = _lib.xrs_replace_batched(self._h, data_base, data_shard_stride, data_stripe_stride,
+                                      _ints(replace_rows), len(replace_rows), size, parity_base,
+                                      parity_shard_stride, parity_stripe_stride, n_stripes, stream)
+        bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)

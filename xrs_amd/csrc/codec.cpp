@@ -1,0 +1,773 @@
+// codec.cpp -- host side of the MI355X X-Reed-Solomon codec and its C ABI.
+//
+// The host owns what xrs.go does on the CPU that is not byte arithmetic:
+// argument checks (xrs.go:130-136, :146-151), the XORSet (xrs.go:77-100),
+// survivor selection and the GF(2^8) matrix inverses of the RS dependency,
+// composition of every operation into one or a few "pair"/"rows" kernel plans
+// (xrs_plan.h), and the per-stripe synchronous API that moves host vects
+// through device staging.  Every byte of shard arithmetic runs in kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "gf256.h"
+#include "xrs_hip.h"
+#include "xrs_plan.h"
+
+using xrs::GF;
+using xrs::GfTab;
+using xrs::RowRef;
+
+struct xrs_codec {
+  int d = 0, p = 0;
+  int device = -1;
+  std::vector<uint8_t> gen;          // (d+p) x d systematic generator
+  std::vector<std::vector<int>> xs;  // xs[h] = XORSet[h] (empty if no such key)
+  std::vector<int> bi_of;            // data j -> parity index whose b-half carries a_j
+  // ReconstOne(k) plans (xrs.go:175-221): survivors has_k = [0..d-1] with k -> d;
+  // r1_bk[k][m] rebuilds b_k, r1_brs[k][m] rebuilds the RS-form b of parity bi.
+  // Built on first use of k (a d x d inverse each), then immutable.
+  mutable std::mutex plan_mu;
+  mutable std::vector<std::vector<uint8_t>> r1_bk, r1_brs;
+
+  // sync-API state (lazy; guarded by mu)
+  mutable std::mutex mu;
+  mutable uint8_t* staging = nullptr;
+  mutable size_t staging_cap = 0;
+  mutable hipStream_t stream = nullptr;
+
+  uint8_t g(int row, int col) const { return gen[static_cast<size_t>(row) * d + col]; }
+};
+
+namespace {
+
+int hip_err(hipError_t e) { return e == hipSuccess ? XRS_OK : XRS_ERR_HIP; }
+
+// ---------------------------------------------------------------- planning
+struct MulSrc {
+  RowRef row;
+  std::vector<uint8_t> coef;  // one per output
+  int pb;                     // pair kernel: output whose b-half takes this a-half, or -1
+};
+struct XorSrc {
+  RowRef row;
+  std::vector<int> outs;  // outputs this row is XORed into
+};
+
+// Pair plans: outputs in groups of kMaxOut, sources in chunks of kMaxSrc; the
+// first chunk of each group writes (or accumulates if acc), later chunks add.
+int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, bool acc,
+             bool encode12, uint64_t half, uint64_t n_stripes, hipStream_t stream) {
+  if (half == 0 || n_stripes == 0 || dst.empty()) return XRS_OK;
+  const GF& gf = GF::get();
+  const int np = static_cast<int>(dst.size()), ns = static_cast<int>(src.size());
+  xrs::PairPlan plan;
+  for (int g0 = 0; g0 < np; g0 += xrs::kMaxOut) {
+    const int P = std::min(xrs::kMaxOut, np - g0);
+    int c0 = 0;
+    do {
+      const int C = std::min(xrs::kMaxSrc, ns - c0);
+      std::memset(&plan, 0, sizeof(plan));
+      plan.P = P;
+      plan.C = C;
+      plan.acc = acc || c0 > 0;
+      plan.encode12 = encode12 && np == 4 && ns == 12;
+      plan.half = half;
+      plan.n_stripes = n_stripes;
+      for (int r = 0; r < P; ++r) plan.dst[r] = dst[g0 + r];
+      for (int c = 0; c < C; ++c) {
+        const MulSrc& s = src[c0 + c];
+        plan.src[c] = s.row;
+        for (int r = 0; r < P; ++r) plan.tab[c][r] = gf.tab(s.coef[g0 + r]);
+        plan.pb[c] = (s.pb >= g0 && s.pb < g0 + P) ? static_cast<int8_t>(s.pb - g0) : -1;
+      }
+      const int e = xrs::launch_pair(plan, stream);
+      if (e != 0) return XRS_ERR_HIP;
+      c0 += C;
+    } while (c0 < ns);
+  }
+  return XRS_OK;
+}
+
+// Rows plans: outputs in groups of kMaxOut; GF and XOR sources in chunks.
+int run_rows(const std::vector<RowRef>& dst, const std::vector<MulSrc>& msrc,
+             const std::vector<XorSrc>& xsrc, bool acc, uint64_t len, uint64_t n_stripes,
+             hipStream_t stream) {
+  if (len == 0 || n_stripes == 0 || dst.empty()) return XRS_OK;
+  const GF& gf = GF::get();
+  const int nr = static_cast<int>(dst.size());
+  xrs::RowsPlan plan;
+  for (int g0 = 0; g0 < nr; g0 += xrs::kMaxOut) {
+    const int R = std::min(xrs::kMaxOut, nr - g0);
+    // XOR sources that touch this group, with their group-relative masks
+    std::vector<std::pair<RowRef, uint32_t>> xs;
+    for (const XorSrc& x : xsrc) {
+      uint32_t m = 0;
+      for (int o : x.outs)
+        if (o >= g0 && o < g0 + R) m ^= 1u << (o - g0);  // ^=: a repeated target cancels
+      if (m) xs.push_back({x.row, m});
+    }
+    const int nm = static_cast<int>(msrc.size()), nx = static_cast<int>(xs.size());
+    int m0 = 0, x0 = 0;
+    bool first = true;
+    do {
+      const int NM = std::min(xrs::kMaxSrc, nm - m0), NX = std::min(xrs::kMaxXor, nx - x0);
+      std::memset(&plan, 0, sizeof(plan));
+      plan.R = R;
+      plan.NM = NM;
+      plan.NX = NX;
+      plan.acc = acc || !first;
+      plan.len = len;
+      plan.n_stripes = n_stripes;
+      for (int r = 0; r < R; ++r) plan.dst[r] = dst[g0 + r];
+      for (int m = 0; m < NM; ++m) {
+        plan.msrc[m] = msrc[m0 + m].row;
+        for (int r = 0; r < R; ++r) plan.tab[m][r] = gf.tab(msrc[m0 + m].coef[g0 + r]);
+      }
+      for (int x = 0; x < NX; ++x) {
+        plan.xsrc[x] = xs[x0 + x].first;
+        plan.xmask[x] = xs[x0 + x].second;
+      }
+      const int e = xrs::launch_rows(plan, stream);
+      if (e != 0) return XRS_ERR_HIP;
+      m0 += NM;
+      x0 += NX;
+      first = false;
+    } while (m0 < nm || x0 < nx);
+  }
+  return XRS_OK;
+}
+
+// Device layout of a batch of stripes.
+struct Layout {
+  uint8_t* base;
+  size_t shard_stride, stripe_stride;
+  RowRef row(int shard, size_t off) const {
+    return {reinterpret_cast<uint64_t>(base) + static_cast<uint64_t>(shard) * shard_stride + off,
+            static_cast<uint64_t>(stripe_stride)};
+  }
+};
+
+int check_size(size_t size) { return (size & 1) ? XRS_ERR_SIZE_NOT_EVEN : XRS_OK; }
+
+int need_vects(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi) {
+  if (k < 0 || k >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;  // xrs.go:148-151
+  *bi = x->bi_of[k];
+  a_need->clear();
+  for (int i : x->xs[*bi])
+    if (i != k) a_need->push_back(i);
+  return XRS_OK;
+}
+
+// Rebuild rows `out` from survivors dp_has[:d] (reedsolomon Reconst [dep]):
+// coefficient row for t = gen[t] * inv(gen[has]).  Validation order follows
+// oracle/xrs_oracle.c oxrs_rs_reconst.
+int survivor_rows(const xrs_codec* x, const int* dp_has, int n_has, const std::vector<int>& out,
+                  std::vector<std::vector<uint8_t>>* coef) {
+  const int d = x->d, n = x->d + x->p;
+  if (out.empty()) return XRS_OK;
+  if (n_has < d) return XRS_ERR_TOO_FEW_SURVIVORS;
+  for (int i = 0; i < n_has; ++i)
+    if (dp_has[i] < 0 || dp_has[i] >= n) return XRS_ERR_ILLEGAL_INDEX;
+  for (int t : out)
+    if (t < 0 || t >= n) return XRS_ERR_ILLEGAL_INDEX;
+  const GF& gf = GF::get();
+  std::vector<uint8_t> e(static_cast<size_t>(d) * d);
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) e[static_cast<size_t>(i) * d + j] = x->g(dp_has[i], j);
+  if (!gf.invert(e, d)) return XRS_ERR_SINGULAR;
+  coef->assign(out.size(), std::vector<uint8_t>(d, 0));
+  for (size_t q = 0; q < out.size(); ++q)
+    for (int i = 0; i < d; ++i) {
+      uint8_t c = 0;
+      for (int j = 0; j < d; ++j) c ^= gf.mul(x->g(out[q], j), e[static_cast<size_t>(j) * d + i]);
+      (*coef)[q][i] = c;
+    }
+  return XRS_OK;
+}
+
+// ReconstOne(k) coefficient rows, built once per (codec, k).
+int reconst_one_plan(const xrs_codec* x, int k, std::vector<uint8_t>* bk,
+                     std::vector<uint8_t>* brs) {
+  std::lock_guard<std::mutex> lk(x->plan_mu);
+  if (x->r1_bk[k].empty()) {
+    std::vector<int> has(x->d);
+    for (int m = 0; m < x->d; ++m) has[m] = m;
+    has[k] = x->d;  // xrs.go:195-199
+    std::vector<std::vector<uint8_t>> coef;
+    const int e = survivor_rows(x, has.data(), x->d, {k, x->bi_of[k]}, &coef);
+    if (e) return e;
+    x->r1_bk[k] = coef[0];
+    x->r1_brs[k] = coef[1];
+  }
+  *bk = x->r1_bk[k];
+  *brs = x->r1_brs[k];
+  return XRS_OK;
+}
+
+// Halves written by a batched op (for the sync API's copy-back).
+struct Written {
+  std::vector<std::pair<int, int>> halves;  // (shard, 0 = a-half / 1 = b-half)
+  void add(int shard, int h) { halves.push_back({shard, h}); }
+};
+
+// ------------------------------------------------------------ batched ops
+int encode_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes,
+                hipStream_t s) {
+  const int d = x->d, p = x->p;
+  const size_t half = size / 2;
+  std::vector<RowRef> dst;
+  for (int r = 0; r < p; ++r) dst.push_back(L.row(d + r, 0));
+  std::vector<MulSrc> src(d);
+  for (int j = 0; j < d; ++j) {
+    src[j].row = L.row(j, 0);
+    src[j].coef.resize(p);
+    for (int r = 0; r < p; ++r) src[j].coef[r] = x->g(d + r, j);
+    src[j].pb = x->bi_of[j] - d;  // xrs.go:118-126 piggyback target
+  }
+  return run_pair(dst, src, false, d == 12 && p == 4, half, n_stripes, s);
+}
+
+int reconst_one_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes, int k,
+                     hipStream_t s) {
+  const int d = x->d;
+  const size_t half = size / 2;
+  std::vector<int> a_need;
+  int bi = 0;
+  int e = need_vects(x, k, &a_need, &bi);
+  if (e) return e;
+  // b_k = sum_m r1_bk[k][m] * b(has_m);  a_k = b(bi) ^ bRS ^ XOR a(aNeed),
+  // bRS = sum_m r1_brs[k][m] * b(has_m)   (xrs.go:205, :213-219)
+  std::vector<uint8_t> bk, brs;
+  if ((e = reconst_one_plan(x, k, &bk, &brs))) return e;
+  std::vector<RowRef> dst = {L.row(k, half), L.row(k, 0)};
+  std::vector<MulSrc> ms(d);
+  for (int m = 0; m < d; ++m) {
+    const int h = (m == k) ? d : m;
+    ms[m].row = L.row(h, half);
+    ms[m].coef = {bk[m], brs[m]};
+    ms[m].pb = -1;
+  }
+  std::vector<XorSrc> xs;
+  xs.push_back({L.row(bi, half), {1}});
+  for (int i : a_need) xs.push_back({L.row(i, 0), {1}});
+  return run_rows(dst, ms, xs, false, half, n_stripes, s);
+}
+
+// xrs.go:236-301 general Reconst: four steps, in the reference's order.
+int reconst_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes,
+                 const int* dp_has, int n_has, const int* need, int n_need, hipStream_t s,
+                 Written* w) {
+  const int d = x->d, p = x->p;
+  const size_t half = size / 2;
+  // Step 1: a-halves of every vect not in dpHas (xrs.go:247-262).
+  std::vector<int> a_lost;
+  for (int i = 0; i < d + p; ++i)
+    if (std::find(dp_has, dp_has + n_has, i) == dp_has + n_has) a_lost.push_back(i);
+  std::vector<std::vector<uint8_t>> coef;
+  int e = survivor_rows(x, dp_has, n_has, a_lost, &coef);
+  if (e) return e;
+  if (!a_lost.empty()) {
+    std::vector<RowRef> dst;
+    for (int t : a_lost) dst.push_back(L.row(t, 0));
+    std::vector<MulSrc> ms(d);
+    for (int m = 0; m < d; ++m) {
+      ms[m].row = L.row(dp_has[m], 0);
+      ms[m].coef.resize(a_lost.size());
+      for (size_t q = 0; q < a_lost.size(); ++q) ms[m].coef[q] = coef[q][m];
+      ms[m].pb = -1;
+    }
+    e = run_rows(dst, ms, {}, false, half, n_stripes, s);
+    if (e) return e;
+    for (int t : a_lost) w->add(t, 0);
+  }
+  // Step 2: retrieveRS, surviving parity h > d back to RS form (xrs.go:305-320).
+  // A repeated h in dpHas is applied repeatedly by the reference: parity of count.
+  {
+    std::vector<int> cnt(d + p, 0);
+    for (int i = 0; i < n_has; ++i)
+      if (dp_has[i] > d && dp_has[i] < d + p) cnt[dp_has[i]] ^= 1;
+    std::vector<RowRef> dst;
+    std::vector<XorSrc> xs;
+    for (int h = d + 1; h < d + p; ++h) {
+      if (!cnt[h] || x->xs[h].empty()) continue;
+      const int o = static_cast<int>(dst.size());
+      dst.push_back(L.row(h, half));
+      for (int ai : x->xs[h]) xs.push_back({L.row(ai, 0), {o}});
+      w->add(h, 1);
+    }
+    if (!dst.empty()) {
+      e = run_rows(dst, {}, xs, true, half, n_stripes, s);
+      if (e) return e;
+    }
+  }
+  // Step 3 + 4: b-halves of need, then re-piggyback needed parity != d
+  // (xrs.go:270-298).  Both write the same rows, so one plan per output.
+  std::vector<int> outs(need, need + n_need);
+  e = survivor_rows(x, dp_has, n_has, outs, &coef);
+  if (e) return e;
+  if (outs.empty()) return XRS_OK;
+  std::vector<int> uniq;  // distinct need rows (a repeated need is rebuilt once)
+  std::vector<int> rep;   // how many times each appears (re-piggyback count)
+  std::vector<size_t> qidx;
+  for (int q = 0; q < n_need; ++q) {
+    auto it = std::find(uniq.begin(), uniq.end(), need[q]);
+    if (it == uniq.end()) {
+      uniq.push_back(need[q]);
+      rep.push_back(1);
+      qidx.push_back(q);
+    } else {
+      rep[it - uniq.begin()]++;
+    }
+  }
+  std::vector<RowRef> dst;
+  for (int t : uniq) dst.push_back(L.row(t, half));
+  std::vector<MulSrc> ms(d);
+  for (int m = 0; m < d; ++m) {
+    ms[m].row = L.row(dp_has[m], half);
+    ms[m].coef.resize(uniq.size());
+    for (size_t u = 0; u < uniq.size(); ++u) ms[m].coef[u] = coef[qidx[u]][m];
+    ms[m].pb = -1;
+  }
+  std::vector<XorSrc> xs;
+  for (size_t u = 0; u < uniq.size(); ++u) {
+    const int t = uniq[u];
+    if (t <= d || (rep[u] & 1) == 0) continue;
+    for (int ai : x->xs[t]) xs.push_back({L.row(ai, 0), {static_cast<int>(u)}});
+  }
+  e = run_rows(dst, ms, xs, false, half, n_stripes, s);
+  if (e) return e;
+  for (int t : uniq) w->add(t, 1);
+  return XRS_OK;
+}
+
+int update_impl(const xrs_codec* x, RowRef old_row, RowRef new_row, size_t size, int row,
+                const Layout& P, size_t n_stripes, hipStream_t s) {
+  const int d = x->d, p = x->p;
+  std::vector<RowRef> dst;
+  for (int r = 0; r < p; ++r) dst.push_back(P.row(r, 0));
+  // Delta = old ^ new is linear: both rows carry the same column of gen
+  // (reedsolomon Update [dep], xrs.go:331) and the same piggyback (:340-344).
+  std::vector<MulSrc> src(2);
+  src[0].row = old_row;
+  src[1].row = new_row;
+  for (auto& sr : src) {
+    sr.coef.resize(p);
+    for (int r = 0; r < p; ++r) sr.coef[r] = x->g(d + r, row);
+    sr.pb = x->bi_of[row] - d;
+  }
+  return run_pair(dst, src, true, false, size / 2, n_stripes, s);
+}
+
+int replace_impl(const xrs_codec* x, const Layout& D, const int* rows, int n, size_t size,
+                 const Layout& P, size_t n_stripes, hipStream_t s) {
+  const int d = x->d, p = x->p;
+  std::vector<RowRef> dst;
+  for (int r = 0; r < p; ++r) dst.push_back(P.row(r, 0));
+  std::vector<MulSrc> src(n);
+  for (int i = 0; i < n; ++i) {
+    src[i].row = D.row(i, 0);
+    src[i].coef.resize(p);
+    for (int r = 0; r < p; ++r) src[i].coef[r] = x->g(d + r, rows[i]);  // xrs.go:370
+    src[i].pb = x->bi_of[rows[i]] - d;                                   // xrs.go:375-385
+  }
+  return run_pair(dst, src, true, false, size / 2, n_stripes, s);
+}
+
+// Replace / Update argument checks (mirror oracle order; row checks before any write).
+int check_replace(const xrs_codec* x, const int* rows, int n, size_t size) {
+  if (n < 1) return XRS_ERR_ILLEGAL_VECTS;
+  int e = check_size(size);
+  if (e) return e;
+  if (n > x->d) return XRS_ERR_ILLEGAL_VECTS;
+  if (!rows) return XRS_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  return XRS_OK;
+}
+
+// ------------------------------------------------------------- sync API
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    if (dev >= 0 && dev != prev_) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+
+ private:
+  int prev_ = -1;
+};
+
+// Ensure the sync stream + `bytes` of staging (caller holds x->mu).
+int ensure_staging(const xrs_codec* x, size_t bytes) {
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  if (!x->stream) {
+    if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess)
+      return XRS_ERR_HIP;
+  }
+  if (bytes > x->staging_cap) {
+    if (x->staging) (void)hipFree(x->staging);
+    x->staging = nullptr;
+    x->staging_cap = 0;
+    size_t cap = std::max<size_t>(bytes, 1 << 20);
+    if (hipMalloc(&x->staging, cap) != hipSuccess) return XRS_ERR_HIP;
+    x->staging_cap = cap;
+  }
+  return XRS_OK;
+}
+
+int h2d(const xrs_codec* x, size_t off, const void* src, size_t n) {
+  if (n == 0) return XRS_OK;
+  if (!src) return XRS_ERR_INVALID_ARG;
+  return hip_err(hipMemcpyAsync(x->staging + off, src, n, hipMemcpyHostToDevice, x->stream));
+}
+int d2h(const xrs_codec* x, void* dst, size_t off, size_t n) {
+  if (n == 0) return XRS_OK;
+  return hip_err(hipMemcpyAsync(dst, x->staging + off, n, hipMemcpyDeviceToHost, x->stream));
+}
+int sync(const xrs_codec* x) { return hip_err(hipStreamSynchronize(x->stream)); }
+
+bool vects_ok(uint8_t* const* v, int n) {
+  if (!v) return false;
+  for (int i = 0; i < n; ++i)
+    if (!v[i]) return false;
+  return true;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* xrs_strerror(int code) {
+  switch (code) {
+    case XRS_OK: return "ok";
+    case XRS_ERR_ILLEGAL_PARITY: return "illegal parity";
+    case XRS_ERR_SIZE_NOT_EVEN: return "vect size not even";
+    case XRS_ERR_ILLEGAL_DATA_INDEX: return "illegal data index";
+    case XRS_ERR_ILLEGAL_VECTS: return "illegal vects";
+    case XRS_ERR_TOO_FEW_SURVIVORS: return "too few survivors";
+    case XRS_ERR_ILLEGAL_INDEX: return "illegal index";
+    case XRS_ERR_SINGULAR: return "singular matrix";
+    case XRS_ERR_HIP: return "hip runtime error";
+    case XRS_ERR_INVALID_ARG: return "invalid argument";
+    case XRS_ERR_NO_DEVICE: return "no gpu device";
+    default: return "unknown error";
+  }
+}
+
+int xrs_format_error(int code, long long arg, char* buf, size_t buflen) {
+  if (!buf || buflen == 0) return 0;
+  int n;
+  if (code == XRS_ERR_SIZE_NOT_EVEN)
+    n = std::snprintf(buf, buflen, "vect size not even: %lld", arg);  // xrs.go:133
+  else if (code == XRS_ERR_ILLEGAL_DATA_INDEX)
+    n = std::snprintf(buf, buflen, "illegal data index: %lld", arg);  // xrs.go:149
+  else
+    n = std::snprintf(buf, buflen, "%s", xrs_strerror(code));
+  return n < 0 ? 0 : n;
+}
+
+const char* xrs_version(void) { return "xrs-hip 0.1 gfx950"; }
+
+// xrs.go:55-68 New + makeXORSet :77-100
+int xrs_new(int data_num, int parity_num, xrs_codec** out) {
+  if (!out) return XRS_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (parity_num == 1) return XRS_ERR_ILLEGAL_PARITY;  // xrs.go:56-59
+  if (data_num <= 0 || parity_num <= 0 || data_num + parity_num > 256) return XRS_ERR_ILLEGAL_VECTS;
+  const GF& gf = GF::get();
+  auto* x = new xrs_codec();
+  const int d = data_num, p = parity_num, n = d + p;
+  x->d = d;
+  x->p = p;
+  x->gen.assign(static_cast<size_t>(n) * d, 0);
+  for (int i = 0; i < d; ++i) x->gen[static_cast<size_t>(i) * d + i] = 1;
+  for (int i = d; i < n; ++i)
+    for (int j = 0; j < d; ++j) x->gen[static_cast<size_t>(i) * d + j] = gf.inv(static_cast<uint8_t>(i ^ j));
+  x->xs.assign(n, {});
+  x->bi_of.assign(d, 0);
+  int j = d + 1;
+  for (int i = 0; i < d; ++i) {
+    if (j > d + p - 1) j = d + 1;
+    x->xs[j].push_back(i);
+    x->bi_of[i] = j;
+    ++j;
+  }
+  x->r1_bk.assign(d, {});  // ReconstOne plans: built on first use of each k
+  x->r1_brs.assign(d, {});
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  int count = 0;
+  if (dev >= 0 && (hipGetDeviceCount(&count) != hipSuccess || count <= 0)) dev = -1;
+  x->device = dev;
+  *out = x;
+  return XRS_OK;
+}
+
+void xrs_free(xrs_codec* x) {
+  if (!x) return;
+  if (x->device >= 0 && (x->stream || x->staging)) {
+    DeviceGuard g(x->device);
+    if (x->stream) (void)hipStreamDestroy(x->stream);
+    if (x->staging) (void)hipFree(x->staging);
+  }
+  delete x;
+}
+
+int xrs_data_num(const xrs_codec* x) { return x ? x->d : XRS_ERR_INVALID_ARG; }
+int xrs_parity_num(const xrs_codec* x) { return x ? x->p : XRS_ERR_INVALID_ARG; }
+
+int xrs_gen_matrix(const xrs_codec* x, uint8_t* out, size_t cap) {
+  if (!x || !out || cap < x->gen.size()) return XRS_ERR_INVALID_ARG;
+  std::memcpy(out, x->gen.data(), x->gen.size());
+  return XRS_OK;
+}
+
+int xrs_xorset(const xrs_codec* x, int parity_index, int* data_idx, int cap, int* len) {
+  if (!x || !len) return XRS_ERR_INVALID_ARG;
+  *len = 0;
+  if (parity_index < 0 || parity_index >= x->d + x->p) return XRS_OK;
+  const auto& v = x->xs[parity_index];
+  if (static_cast<int>(v.size()) > cap || (!data_idx && !v.empty())) return XRS_ERR_INVALID_ARG;
+  for (size_t i = 0; i < v.size(); ++i) data_idx[i] = v[i];
+  *len = static_cast<int>(v.size());
+  return XRS_OK;
+}
+
+// xrs.go:146-171
+int xrs_get_need_vects(const xrs_codec* x, int k, int* a_need, int* a_len, int b_need[2]) {
+  if (!x || !a_len || !b_need) return XRS_ERR_INVALID_ARG;
+  std::vector<int> an;
+  int bi = 0;
+  const int e = need_vects(x, k, &an, &bi);
+  if (e) return e;
+  if (!a_need && !an.empty()) return XRS_ERR_INVALID_ARG;
+  for (size_t i = 0; i < an.size(); ++i) a_need[i] = an[i];
+  *a_len = static_cast<int>(an.size());
+  b_need[0] = x->d;
+  b_need[1] = bi;
+  return XRS_OK;
+}
+
+// ---------------------------------------------------------------- batched
+int xrs_encode_batched(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                       size_t stripe_stride, size_t n_stripes, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  return encode_impl(x, {base, shard_stride, stripe_stride}, size, n_stripes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int xrs_reconst_one_batched(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                            size_t stripe_stride, size_t n_stripes, int k, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (k < 0 || k >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  return reconst_one_impl(x, {base, shard_stride, stripe_stride}, size, n_stripes, k,
+                          static_cast<hipStream_t>(stream));
+}
+
+int xrs_reconst_batched(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                        size_t stripe_stride, size_t n_stripes, const int* dp_has, int n_has,
+                        const int* need, int n_need, void* stream) {
+  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] < x->d)  // xrs.go:238-240
+    return xrs_reconst_one_batched(x, base, size, shard_stride, stripe_stride, n_stripes, need[0],
+                                   stream);
+  int e = check_size(size);
+  if (e) return e;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  Written w;
+  const size_t ns = (size == 0 || !base) ? 0 : n_stripes;
+  return reconst_impl(x, {base, shard_stride, stripe_stride}, size, ns, dp_has, n_has, need,
+                      n_need, static_cast<hipStream_t>(stream), &w);
+}
+
+int xrs_update_batched(const xrs_codec* x, const uint8_t* old_base, size_t old_stripe_stride,
+                       const uint8_t* new_base, size_t new_stripe_stride, size_t size, int row,
+                       uint8_t* parity_base, size_t parity_shard_stride,
+                       size_t parity_stripe_stride, size_t n_stripes, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (row < 0 || row >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!old_base || !new_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const RowRef o{reinterpret_cast<uint64_t>(old_base), old_stripe_stride};
+  const RowRef nw{reinterpret_cast<uint64_t>(new_base), new_stripe_stride};
+  return update_impl(x, o, nw, size, row, {parity_base, parity_shard_stride, parity_stripe_stride},
+                     n_stripes, static_cast<hipStream_t>(stream));
+}
+
+int xrs_replace_batched(const xrs_codec* x, const uint8_t* data_base, size_t data_shard_stride,
+                        size_t data_stripe_stride, const int* rows, int n, size_t size,
+                        uint8_t* parity_base, size_t parity_shard_stride,
+                        size_t parity_stripe_stride, size_t n_stripes, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_replace(x, rows, n, size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!data_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  return replace_impl(x, {const_cast<uint8_t*>(data_base), data_shard_stride, data_stripe_stride},
+                      rows, n, size, {parity_base, parity_shard_stride, parity_stripe_stride},
+                      n_stripes, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------- sync
+// xrs.go:103-128
+int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  if (n < 1) return XRS_ERR_ILLEGAL_VECTS;
+  int e = check_size(size);
+  if (e) return e;
+  if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
+  if (size == 0) return XRS_OK;
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  if ((e = ensure_staging(x, static_cast<size_t>(n) * size))) return e;
+  for (int j = 0; j < x->d && !e; ++j) e = h2d(x, static_cast<size_t>(j) * size, vects[j], size);
+  if (!e) e = encode_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size, 1, x->stream);
+  for (int r = 0; r < x->p && !e; ++r)
+    e = d2h(x, vects[x->d + r], static_cast<size_t>(x->d + r) * size, size);
+  const int es = sync(x);
+  return e ? e : es;
+}
+
+// xrs.go:175-221: only the GetNeedVects set travels to the device.
+int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, int k) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  std::vector<int> a_need;
+  int bi = 0;
+  if ((e = need_vects(x, k, &a_need, &bi))) return e;
+  if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!vects) return XRS_ERR_INVALID_ARG;
+  if (size == 0) return XRS_OK;
+  const int d = x->d;
+  const size_t half = size / 2;
+  std::vector<std::pair<int, int>> reads;  // (shard, half)
+  for (int m = 0; m < d; ++m) reads.push_back({m == k ? d : m, 1});
+  reads.push_back({bi, 1});
+  for (int i : a_need) reads.push_back({i, 0});
+  for (auto& r : reads)
+    if (!vects[r.first]) return XRS_ERR_INVALID_ARG;
+  if (!vects[k]) return XRS_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  if ((e = ensure_staging(x, static_cast<size_t>(n) * size))) return e;
+  for (size_t i = 0; i < reads.size() && !e; ++i) {
+    const size_t off = static_cast<size_t>(reads[i].first) * size + reads[i].second * half;
+    e = h2d(x, off, vects[reads[i].first] + reads[i].second * half, half);
+  }
+  if (!e) e = reconst_one_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size, 1, k, x->stream);
+  if (!e) e = d2h(x, vects[k], static_cast<size_t>(k) * size, size);
+  const int es = sync(x);
+  return e ? e : es;
+}
+
+// xrs.go:236-301
+int xrs_reconst(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, const int* dp_has,
+                int n_has, const int* need, int n_need) {
+  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] < x->d) return xrs_reconst_one(x, vects, n, size, need[0]);
+  int e = check_size(size);
+  if (e) return e;
+  if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  if ((e = ensure_staging(x, std::max<size_t>(1, static_cast<size_t>(n) * size)))) return e;
+  for (int i = 0; i < n && !e; ++i) e = h2d(x, static_cast<size_t>(i) * size, vects[i], size);
+  if (e) {
+    (void)sync(x);
+    return e;
+  }
+  Written w;
+  const int er = reconst_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size,
+                              size ? 1 : 0, dp_has, n_has, need, n_need, x->stream, &w);
+  // Copy back every half the device wrote, also when a later step failed
+  // (the reference's Reconst is not atomic either).
+  const size_t half = size / 2;
+  for (auto& h : w.halves) {
+    if (e) break;
+    e = d2h(x, vects[h.first] + h.second * half,
+            static_cast<size_t>(h.first) * size + h.second * half, half);
+  }
+  const int es = sync(x);
+  return er ? er : (e ? e : es);
+}
+
+// xrs.go:324-346
+int xrs_update(const xrs_codec* x, const uint8_t* old_data, const uint8_t* new_data, size_t size,
+               int row, uint8_t* const* parity, int n_parity) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (row < 0 || row >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_parity != x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!old_data || !new_data || !vects_ok(parity, n_parity)) return XRS_ERR_INVALID_ARG;
+  if (size == 0) return XRS_OK;
+  const int p = x->p;
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  // staging rows: [0, p) parity, p old, p+1 new
+  const size_t stride = static_cast<size_t>(p + 2) * size;
+  if ((e = ensure_staging(x, stride))) return e;
+  for (int r = 0; r < p && !e; ++r) e = h2d(x, static_cast<size_t>(r) * size, parity[r], size);
+  if (!e) e = h2d(x, static_cast<size_t>(p) * size, old_data, size);
+  if (!e) e = h2d(x, static_cast<size_t>(p + 1) * size, new_data, size);
+  const Layout P{x->staging, size, stride};
+  if (!e) e = update_impl(x, P.row(p, 0), P.row(p + 1, 0), size, row, P, 1, x->stream);
+  for (int r = 0; r < p && !e; ++r) e = d2h(x, parity[r], static_cast<size_t>(r) * size, size);
+  const int es = sync(x);
+  return e ? e : es;
+}
+
+// xrs.go:363-387
+int xrs_replace(const xrs_codec* x, uint8_t* const* data, const int* rows, int n, size_t size,
+                uint8_t* const* parity, int n_parity) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_replace(x, rows, n, size);
+  if (e) return e;
+  if (n_parity != x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!vects_ok(data, n) || !vects_ok(parity, n_parity)) return XRS_ERR_INVALID_ARG;
+  if (size == 0) return XRS_OK;
+  const int p = x->p;
+  std::lock_guard<std::mutex> lk(x->mu);
+  DeviceGuard g(x->device);
+  // staging rows: [0, p) parity, [p, p+n) data
+  const size_t stride = static_cast<size_t>(p + n) * size;
+  if ((e = ensure_staging(x, stride))) return e;
+  for (int r = 0; r < p && !e; ++r) e = h2d(x, static_cast<size_t>(r) * size, parity[r], size);
+  for (int i = 0; i < n && !e; ++i) e = h2d(x, static_cast<size_t>(p + i) * size, data[i], size);
+  const Layout P{x->staging, size, stride};
+  const Layout D{x->staging + static_cast<size_t>(p) * size, size, stride};
+  if (!e) e = replace_impl(x, D, rows, n, size, P, 1, x->stream);
+  for (int r = 0; r < p && !e; ++r) e = d2h(x, parity[r], static_cast<size_t>(r) * size, size);
+  const int es = sync(x);
+  return e ? e : es;
+}
+
+}  // extern "C"

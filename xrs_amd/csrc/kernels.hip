@@ -1,0 +1,452 @@
+// kernels.hip -- gfx950 (MI355X, CDNA4) kernels for the X-Reed-Solomon codec.
+//
+// Hot path of templexxx/xrs: the GF(2^8) Cauchy multiply-accumulate over shard
+// bytes (reedsolomon RS.Encode/Reconst/Update/Replace, called from
+// /root/reference/xrs.go:112,205,259,275,331,370) plus the a/b-half piggyback
+// XOR (xorsimd call sites xrs.go:125,219,295,316,344,383).
+//
+// Design (DESIGN.md has the roofline arithmetic):
+//  * Pure HBM streaming, integer VALU work; no MFMA and no LDS on the data path.
+//  * Each lane owns 16 bytes at offset o of the a-half AND the same 16 bytes of
+//    the b-half (o + H) of every row it touches, so the piggyback XOR uses a-half
+//    bytes the lane already holds: RS + piggyback is one pass over HBM.
+//  * Loads/stores are global_load/store_dwordx4: one wave moves 1 KiB
+//    contiguous per instruction per row (full 128-B lines).
+//  * GF multiply by a constant c = three v_perm_b32 byte lookups (8-, 8- and
+//    4-entry tables indexed by bits 0-2, 3-5, 6-7) XORed with v_bitop3_b32.
+//    One v_perm looks up 4 bytes; the table dwords come from kernel-argument
+//    SGPRs (gfx950 allows one SGPR operand per VALU op, the other half of an
+//    8-entry table is moved to a VGPR once per 16 bytes).
+//  * The headline shapes (12+4 Encode, 12+4 ReconstOne) are compile-time so
+//    every load is in flight before the first multiply; other shapes use
+//    runtime-count variants.  Misaligned / odd sizes take a byte-granular path.
+#include <hip/hip_runtime.h>
+
+#include "xrs_plan.h"
+
+namespace xrs {
+namespace {
+
+constexpr int kDyn = -1;  // count known only at run time
+constexpr int kBlock = 256;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c
+}
+
+struct Sel {
+  uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel sel_of(uint32_t x) {
+  return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+
+// c * x on four bytes.  v_perm_b32(S0=hi, S1=lo, sel): selector byte 0..3 picks
+// a byte of lo, 4..7 a byte of hi.
+__device__ __forceinline__ uint32_t gmul(const GfTab& t, const Sel& s) {
+  return x3(__builtin_amdgcn_perm(t.hi0, t.lo0, s.s0), __builtin_amdgcn_perm(t.hi1, t.lo1, s.s1),
+            __builtin_amdgcn_perm(0u, t.top, s.s2));
+}
+
+// ---- fragment load/store: W dwords per lane per row ------------------------
+// VEC: one 16-byte dwordx4 access (address 16-byte aligned).
+// !VEC: nb (1..4) single-byte accesses (any alignment, ragged tail).
+template <bool VEC>
+__device__ __forceinline__ void ld(uint32_t* v, uint64_t addr, int nb) {
+  if constexpr (VEC) {
+    const u32x4 t = *reinterpret_cast<const u32x4*>(addr);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  } else {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(addr);
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < nb) x |= static_cast<uint32_t>(p[i]) << (8 * i);
+    v[0] = x;
+  }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void st(const uint32_t* v, uint64_t addr, int nb) {
+  if constexpr (VEC) {
+    u32x4 t;
+    t.x = v[0];
+    t.y = v[1];
+    t.z = v[2];
+    t.w = v[3];
+    *reinterpret_cast<u32x4*>(addr) = t;
+  } else {
+    uint8_t* p = reinterpret_cast<uint8_t*>(addr);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < nb) p[i] = static_cast<uint8_t>(v[0] >> (8 * i));
+  }
+}
+
+__device__ __forceinline__ uint64_t row_addr(const RowRef& r, uint64_t stripe, uint64_t off) {
+  return r.ptr + stripe * r.stripe_stride + off;
+}
+
+// ============================================================ pair kernel
+// Encode / Replace / Update:  for o in [0, H):
+//   dst_r[o]   (^)= sum_c coef[c][r] * src_c[o]
+//   dst_r[H+o] (^)= sum_c coef[c][r] * src_c[H+o]  ^  XOR_{c: pb[c]==r} src_c[o]
+template <int P, int C, bool VEC>
+struct PairArgs {
+  static constexpr int CM = C == kDyn ? kMaxSrc : C;
+  GfTab tab[CM][P];
+  RowRef src[CM];
+  RowRef dst[P];
+  uint32_t pbmask[P];  // bit c: XOR src_c's a-half into dst_r's b-half
+  int n_src;
+  uint64_t half;    // H
+  uint64_t chunks;  // lanes per stripe
+  uint64_t total;   // n_stripes * chunks
+};
+
+template <int P, int W>
+__device__ __forceinline__ void pair_mac1(uint32_t (&acc_a)[P][W], uint32_t (&acc_b)[P][W],
+                                          const GfTab* tab, const uint32_t* xa,
+                                          const uint32_t* xb) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const Sel sa = sel_of(xa[w]), sb = sel_of(xb[w]);
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      acc_a[r][w] ^= gmul(tab[r], sa);
+      acc_b[r][w] ^= gmul(tab[r], sb);
+    }
+  }
+}
+
+template <int P, int W>
+__device__ __forceinline__ void pair_mac2(uint32_t (&acc_a)[P][W], uint32_t (&acc_b)[P][W],
+                                          const GfTab* tab0, const GfTab* tab1,
+                                          const uint32_t* xa0, const uint32_t* xb0,
+                                          const uint32_t* xa1, const uint32_t* xb1) {
+  // Selectors for all W dwords of both sources first, then one output at a
+  // time: each table dword moved to a VGPR is reused 2*W times.
+  Sel sa0[W], sb0[W], sa1[W], sb1[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    sa0[w] = sel_of(xa0[w]);
+    sb0[w] = sel_of(xb0[w]);
+    sa1[w] = sel_of(xa1[w]);
+    sb1[w] = sel_of(xb1[w]);
+  }
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      acc_a[r][w] = x3(acc_a[r][w], gmul(tab0[r], sa0[w]), gmul(tab1[r], sa1[w]));
+      acc_b[r][w] = x3(acc_b[r][w], gmul(tab0[r], sb0[w]), gmul(tab1[r], sb1[w]));
+    }
+  }
+}
+
+// acc ^= x & m  (m = all-ones or zero, wave-uniform): one v_bitop3, no branch
+// (a branch per output lets the compiler turn the chain into a dynamically
+// indexed accumulator array, which lands in scratch).
+__device__ __forceinline__ uint32_t xor_masked(uint32_t acc, uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(acc, x, m, 0x78);  // a ^ (b & c)
+}
+
+// Piggyback of source c (runtime pattern): output r takes src_c's a-half if
+// bit c of pbmask[r] is set.
+template <int P, int W>
+__device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_t* pbmask, int c,
+                                          const uint32_t* xa) {
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const uint32_t m = 0u - ((pbmask[r] >> c) & 1u);
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc_b[r][w] = xor_masked(acc_b[r][w], xa[w], m);
+  }
+}
+
+template <int P, int C, bool ACC, bool VEC>
+__global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> a) {
+  constexpr int W = VEC ? 4 : 1;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
+
+  uint32_t acc_a[P][W], acc_b[P][W];
+  if constexpr (ACC) {
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const uint64_t d = row_addr(a.dst[r], stripe, off);
+      ld<VEC>(acc_a[r], d, nb);
+      ld<VEC>(acc_b[r], d + a.half, nb);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc_a[r][w] = acc_b[r][w] = 0u;
+  }
+
+  if constexpr (C != kDyn) {
+    // Compile-time source count: every load issued up front.
+    uint32_t xa[C][W], xb[C][W];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const uint64_t s = row_addr(a.src[c], stripe, off);
+      ld<VEC>(xa[c], s, nb);
+      ld<VEC>(xb[c], s + a.half, nb);
+    }
+#pragma unroll
+    for (int c = 0; c + 1 < C; c += 2)
+      pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
+    if constexpr (C & 1) pair_mac1<P, W>(acc_a, acc_b, a.tab[C - 1], xa[C - 1], xb[C - 1]);
+    // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
+    // c rides on parity 1 + c % (P-1).  Only used for full-width Encode.
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+  } else {
+    for (int c = 0; c < a.n_src; ++c) {
+      uint32_t xa[W], xb[W];
+      const uint64_t s = row_addr(a.src[c], stripe, off);
+      ld<VEC>(xa, s, nb);
+      ld<VEC>(xb, s + a.half, nb);
+      pair_mac1<P, W>(acc_a, acc_b, a.tab[c], xa, xb);
+      piggyback<P, W>(acc_b, a.pbmask, c, xa);
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const uint64_t d = row_addr(a.dst[r], stripe, off);
+    st<VEC>(acc_a[r], d, nb);
+    st<VEC>(acc_b[r], d + a.half, nb);
+  }
+}
+
+// ============================================================ rows kernel
+// ReconstOne / Reconst steps / retrieveRS:  for o in [0, len):
+//   dst_r[o] (^)= sum_m coef[m][r] * msrc_m[o]  ^  XOR_{x: xmask[x]>>r & 1} xsrc_x[o]
+template <int R, int NM, int NX, bool VEC>
+struct RowsArgs {
+  static constexpr int MM = NM == kDyn ? kMaxSrc : (NM > 0 ? NM : 1);
+  static constexpr int XM = NX == kDyn ? kMaxXor : (NX > 0 ? NX : 1);
+  GfTab tab[MM][R];
+  RowRef msrc[MM];
+  RowRef xsrc[XM];
+  uint32_t xmask[XM];
+  RowRef dst[R];
+  int nm, nx;
+  uint64_t len;
+  uint64_t chunks;
+  uint64_t total;
+};
+
+template <int R, int W>
+__device__ __forceinline__ void rows_mac1(uint32_t (&acc)[R][W], const GfTab* tab,
+                                          const uint32_t* x) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const Sel s = sel_of(x[w]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][w] ^= gmul(tab[r], s);
+  }
+}
+
+template <int R, int W>
+__device__ __forceinline__ void rows_mac2(uint32_t (&acc)[R][W], const GfTab* tab0,
+                                          const GfTab* tab1, const uint32_t* x0,
+                                          const uint32_t* x1) {
+  Sel s0[W], s1[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    s0[w] = sel_of(x0[w]);
+    s1[w] = sel_of(x1[w]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = x3(acc[r][w], gmul(tab0[r], s0[w]), gmul(tab1[r], s1[w]));
+}
+
+template <int R, int W>
+__device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, const uint32_t* x) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t m = 0u - ((mask >> r) & 1u);
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = xor_masked(acc[r][w], x[w], m);
+  }
+}
+
+template <int R, int NM, int NX, bool ACC, bool VEC>
+__global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
+  constexpr int W = VEC ? 4 : 1;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
+
+  uint32_t acc[R][W];
+  if constexpr (ACC) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) ld<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+  }
+
+  if constexpr (NM != kDyn && NX != kDyn) {
+    uint32_t xm[NM > 0 ? NM : 1][W], xx[NX > 0 ? NX : 1][W];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) ld<VEC>(xm[m], row_addr(a.msrc[m], stripe, off), nb);
+#pragma unroll
+    for (int x = 0; x < NX; ++x) ld<VEC>(xx[x], row_addr(a.xsrc[x], stripe, off), nb);
+#pragma unroll
+    for (int m = 0; m + 1 < NM; m += 2) rows_mac2<R, W>(acc, a.tab[m], a.tab[m + 1], xm[m], xm[m + 1]);
+    if constexpr (NM & 1) rows_mac1<R, W>(acc, a.tab[NM - 1], xm[NM - 1]);
+#pragma unroll
+    for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
+  } else {
+    for (int m = 0; m < a.nm; ++m) {
+      uint32_t v[W];
+      ld<VEC>(v, row_addr(a.msrc[m], stripe, off), nb);
+      rows_mac1<R, W>(acc, a.tab[m], v);
+    }
+    for (int x = 0; x < a.nx; ++x) {
+      uint32_t v[W];
+      ld<VEC>(v, row_addr(a.xsrc[x], stripe, off), nb);
+      rows_xor<R, W>(acc, a.xmask[x], v);
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
+}
+
+// ============================================================ launchers
+inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+template <int P, int C, bool ACC, bool VEC>
+int launch_pair_t(const PairPlan& p, hipStream_t stream) {
+  PairArgs<P, C, VEC> a;
+  const int n = p.C;
+  for (int c = 0; c < n; ++c) {
+    for (int r = 0; r < P; ++r) a.tab[c][r] = p.tab[c][r];
+    a.src[c] = p.src[c];
+  }
+  for (int r = 0; r < P; ++r) {
+    a.dst[r] = p.dst[r];
+    a.pbmask[r] = 0;
+  }
+  for (int c = 0; c < n; ++c)
+    if (p.pb[c] >= 0) a.pbmask[p.pb[c]] |= 1u << c;
+  a.n_src = n;
+  a.half = p.half;
+  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.total = a.chunks * p.n_stripes;
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int P, bool ACC, bool VEC>
+int launch_pair_c(const PairPlan& p, hipStream_t s) {
+  if constexpr (P == 4 && !ACC) {
+    if (p.C == 12 && p.encode12) return launch_pair_t<4, 12, ACC, VEC>(p, s);  // 12+4 Encode
+  }
+  return launch_pair_t<P, kDyn, ACC, VEC>(p, s);
+}
+
+template <bool ACC, bool VEC>
+int launch_pair_p(const PairPlan& p, hipStream_t s) {
+  switch (p.P) {
+    case 1: return launch_pair_c<1, ACC, VEC>(p, s);
+    case 2: return launch_pair_c<2, ACC, VEC>(p, s);
+    case 3: return launch_pair_c<3, ACC, VEC>(p, s);
+    case 4: return launch_pair_c<4, ACC, VEC>(p, s);
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+}
+
+template <int R, int NM, int NX, bool ACC, bool VEC>
+int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
+  RowsArgs<R, NM, NX, VEC> a;
+  for (int m = 0; m < p.NM; ++m) {
+    for (int r = 0; r < R; ++r) a.tab[m][r] = p.tab[m][r];
+    a.msrc[m] = p.msrc[m];
+  }
+  for (int x = 0; x < p.NX; ++x) {
+    a.xsrc[x] = p.xsrc[x];
+    a.xmask[x] = p.xmask[x];
+  }
+  for (int r = 0; r < R; ++r) a.dst[r] = p.dst[r];
+  a.nm = p.NM;
+  a.nx = p.NX;
+  a.len = p.len;
+  a.chunks = VEC ? p.len / 16 : (p.len + 3) / 4;
+  a.total = a.chunks * p.n_stripes;
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int R, bool ACC, bool VEC>
+int launch_rows_c(const RowsPlan& p, hipStream_t s) {
+  if constexpr (R == 2 && !ACC) {
+    if (p.NM == 12 && p.NX == 4) return launch_rows_t<2, 12, 4, ACC, VEC>(p, s);  // 12+4 ReconstOne
+  }
+  return launch_rows_t<R, kDyn, kDyn, ACC, VEC>(p, s);
+}
+
+template <bool ACC, bool VEC>
+int launch_rows_r(const RowsPlan& p, hipStream_t s) {
+  switch (p.R) {
+    case 1: return launch_rows_c<1, ACC, VEC>(p, s);
+    case 2: return launch_rows_c<2, ACC, VEC>(p, s);
+    case 3: return launch_rows_c<3, ACC, VEC>(p, s);
+    case 4: return launch_rows_c<4, ACC, VEC>(p, s);
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+}
+
+}  // namespace
+
+int launch_pair(const PairPlan& p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.P < 1 || p.P > kMaxOut || p.C < 0 || p.C > kMaxSrc) return static_cast<int>(hipErrorInvalidValue);
+  bool vec = aligned16(p.half);
+  for (int c = 0; c < p.C && vec; ++c) vec = aligned16(p.src[c].ptr) && aligned16(p.src[c].stripe_stride);
+  for (int r = 0; r < p.P && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
+  if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
+  return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
+}
+
+int launch_rows(const RowsPlan& p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.R < 1 || p.R > kMaxOut || p.NM < 0 || p.NM > kMaxSrc || p.NX < 0 || p.NX > kMaxXor)
+    return static_cast<int>(hipErrorInvalidValue);
+  bool vec = aligned16(p.len);
+  for (int m = 0; m < p.NM && vec; ++m) vec = aligned16(p.msrc[m].ptr) && aligned16(p.msrc[m].stripe_stride);
+  for (int x = 0; x < p.NX && vec; ++x) vec = aligned16(p.xsrc[x].ptr) && aligned16(p.xsrc[x].stripe_stride);
+  for (int r = 0; r < p.R && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
+  if (p.acc) return vec ? launch_rows_r<true, true>(p, s) : launch_rows_r<true, false>(p, s);
+  return vec ? launch_rows_r<false, true>(p, s) : launch_rows_r<false, false>(p, s);
+}
+
+}  // namespace xrs

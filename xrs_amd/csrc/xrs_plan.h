@@ -1,0 +1,74 @@
+// xrs_plan.h -- launch plans shared by the host planner (codec.cpp) and the
+// gfx950 kernels (kernels.hip).  Internal; not part of the C ABI.
+//
+// Two kernel shapes cover the whole xrs.go API surface:
+//
+//  * "pair" kernel  (Encode xrs.go:103, Replace :363, Update :324):
+//      for every byte offset o of the a-half (H = size/2):
+//        dst_r[o]   (^)= sum_c coef[c][r] * src_c[o]
+//        dst_r[H+o] (^)= sum_c coef[c][r] * src_c[H+o]  ^  XOR_{c: pb[c]==r} src_c[o]
+//    i.e. the RS matrix on both halves plus the piggyback XOR (xrs.go:118-126)
+//    in ONE pass over HBM (the reference makes two).
+//
+//  * "rows" kernel  (ReconstOne xrs.go:175, the 4 steps of Reconst :236,
+//    retrieveRS :305):
+//      dst_r[o] (^)= sum_{m<NM} coef[m][r] * msrc_m[o]  ^  XOR_{x: xmask[x]>>r&1} xsrc_x[o]
+//    over arbitrary half-rows (a row = one half of one shard).
+//
+// A row is addressed as ptr + stripe * stripe_stride (+ o); ptr is a device
+// address.  GF(2^8) multiply by a constant c is done with three v_perm_b32
+// byte lookups (see GfTab) so every coefficient is a 20-byte table.
+#pragma once
+#include <stdint.h>
+
+namespace xrs {
+
+// Per-coefficient byte-permute tables.  For x = b7..b0:
+//   c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]
+// T0/T1 have 8 one-byte entries (two dwords: lo = entries 0..3, hi = 4..7),
+// T2 has 4 (one dword).  v_perm_b32 looks up 4 bytes at once.
+struct GfTab {
+  uint32_t lo0, hi0, lo1, hi1, top;
+};
+
+struct RowRef {
+  uint64_t ptr;            // device address of this row in stripe 0
+  uint64_t stripe_stride;  // bytes between consecutive stripes
+};
+
+constexpr int kMaxOut = 4;   // outputs per launch (parity rows / rebuilt rows)
+constexpr int kMaxSrc = 24;  // GF sources per launch (more: chained ACC launches)
+constexpr int kMaxXor = 24;  // XOR-only sources per launch (rows kernel)
+
+struct PairPlan {
+  int P;             // outputs (<= kMaxOut)
+  int C;             // sources (<= kMaxSrc)
+  bool acc;          // true: XOR into existing dst (Replace/Update, chained chunks)
+  GfTab tab[kMaxSrc][kMaxOut];
+  RowRef src[kMaxSrc];
+  RowRef dst[kMaxOut];
+  int8_t pb[kMaxSrc];  // piggyback target output of source c's a-half, or -1
+  bool encode12;       // pb follows the 12+4 XORSet (source c = data c): hot kernel
+  uint64_t half;       // H = size/2 bytes
+  uint64_t n_stripes;
+};
+
+struct RowsPlan {
+  int R;   // outputs (<= kMaxOut)
+  int NM;  // GF sources (<= kMaxSrc)
+  int NX;  // XOR sources (<= kMaxXor)
+  bool acc;
+  GfTab tab[kMaxSrc][kMaxOut];
+  RowRef msrc[kMaxSrc];
+  RowRef xsrc[kMaxXor];
+  uint32_t xmask[kMaxXor];  // bit r set: XOR xsrc into output r
+  RowRef dst[kMaxOut];
+  uint64_t len;  // bytes per row
+  uint64_t n_stripes;
+};
+
+// Kernel launchers (kernels.hip).  Return a hipError_t value as int.
+int launch_pair(const PairPlan& plan, void* stream);
+int launch_rows(const RowsPlan& plan, void* stream);
+
+}  // namespace xrs

@@ -128,11 +128,15 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     n_enc, n_rec = args.enc_stripes, args.rec_stripes
-    enc_buf = torch.randint(0, 256, (n_enc * (D + P) * ENC_S,), dtype=torch.uint8, device=dev,
+    # Device batch layout: the library's recommended strides (xrs_batch_strides):
+    # 4 KiB vects back to back, 1 MiB vects with a 256 B pad per shard.
+    enc_shard, enc_stripe = xrs_amd.batch_strides(ENC_S, D + P)
+    rec_shard, rec_stripe = xrs_amd.batch_strides(REC_S, D + P)
+    enc_buf = torch.randint(0, 256, (n_enc * enc_stripe,), dtype=torch.uint8, device=dev,
                             generator=g)
-    rec_buf = torch.randint(0, 256, (n_rec * (D + P) * REC_S,), dtype=torch.uint8, device=dev,
+    rec_buf = torch.randint(0, 256, (n_rec * rec_stripe,), dtype=torch.uint8, device=dev,
                             generator=g)
-    x.encode_batched(rec_buf.data_ptr(), REC_S, REC_S, (D + P) * REC_S, n_rec, stream)
+    x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, stream)
     torch.cuda.synchronize()
     enc_bytes = n_enc * (D + P) * ENC_S          # per launch, algorithmic (read + write)
     rec_bytes = n_rec * 9 * REC_S
@@ -143,11 +147,11 @@ def main():
         if events:
             events[0].record()
         if n_enc:
-            x.encode_batched(enc_buf.data_ptr(), ENC_S, ENC_S, (D + P) * ENC_S, n_enc, stream)
+            x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
         if events:
             events[1].record()
         if n_rec:
-            x.reconst_one_batched(rec_buf.data_ptr(), REC_S, REC_S, (D + P) * REC_S, n_rec,
+            x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
                                   i % D, stream)
         if events:
             events[2].record()
@@ -225,6 +229,7 @@ def main():
                 "data_shards": D, "parity_shards": P,
                 "encode_vect_bytes": ENC_S, "encode_stripes_per_gpu": n_enc,
                 "reconst_vect_bytes": REC_S, "reconst_stripes_per_gpu": n_rec,
+                "encode_shard_stride": enc_shard, "reconst_shard_stride": rec_shard,
                 "parallelism": f"stripe split x{world}, no collective",
             },
             "kernels": kernels,

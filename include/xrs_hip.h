@@ -91,6 +91,11 @@ int xrs_replace(const xrs_codec *codec, uint8_t *const *data, const int *rows, i
                 size_t size, uint8_t *const *parity, int n_parity);
 
 /* ---- batched, device-resident, async (the performance path) ----------- */
+/* Recommended device layout for a batch of stripes of n_shards vects of
+ * `size` bytes: shard stride (size + pad) and stripe stride.  The pad keeps
+ * rows of large power-of-two sizes off the same HBM channels (measured on
+ * MI355X, DESIGN.md "Layout"); any layout works, this one streams fastest. */
+int xrs_batch_strides(size_t size, int n_shards, size_t *shard_stride, size_t *stripe_stride);
 /* Encode n_stripes stripes in place.  One fused pass: RS + piggyback. */
 int xrs_encode_batched(const xrs_codec *codec, uint8_t *base, size_t size,
                        size_t shard_stride, size_t stripe_stride, size_t n_stripes,

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Turn two rocprofv3 --pmc passes of bench.py into HBM bytes per launch.
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- \
+        python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- \
+        python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/pmc_traffic.json
+
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md "HBM"): FETCH_SIZE and
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a
+16-B-per-lane coalesced streaming read, so it is doubled; WRITE_SIZE is exact
+for 16-B-per-lane stores.  Counters are per dispatch; the bench's timed
+launches are told apart from the setup encode by grid size.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# bench.py kernel keys -> (kernel-name fragment, grid threads of the timed launch)
+KERNELS = {
+    "encode_4k": ("pair_kernel<4, 12, false, true>", 65536 * 128),
+    "reconst_one_1m": ("rows_kernel<2, 12, 4, false, true>", 512 * 32768),
+}
+ALGO_BYTES = {"encode_4k": 65536 * 16 * 4096, "reconst_one_1m": 512 * 9 * (1 << 20)}
+
+
+def read_counter(d, counter):
+    vals = defaultdict(list)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row.get("Kernel_Name", "")
+            grid = int(float(row.get("Grid_Size", row.get("Grid_Size_X", 0)) or 0))
+            for key, (frag, g) in KERNELS.items():
+                if frag in name and grid == g:
+                    vals[key].append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    fetch_dir, write_dir = sys.argv[1], sys.argv[2]
+    fetch = read_counter(fetch_dir, "FETCH_SIZE")
+    write = read_counter(write_dir, "WRITE_SIZE")
+    out = {}
+    for key in KERNELS:
+        if not fetch.get(key) or not write.get(key):
+            continue
+        f = sum(fetch[key]) / len(fetch[key]) * 1024 * 2  # KiB, gfx950 half-count
+        w = sum(write[key]) / len(write[key]) * 1024
+        out[key] = {
+            "fetch_bytes_per_launch": int(f), "write_bytes_per_launch": int(w),
+            "hbm_bytes_per_launch": int(f + w),
+            "algorithmic_bytes_per_launch": ALGO_BYTES[key],
+            "ratio_to_algorithmic": round((f + w) / ALGO_BYTES[key], 4),
+            "launches": [len(fetch[key]), len(write[key])],
+            "correction": "FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (gfx950, MI355X_MICROARCH.md HBM)",
+        }
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()

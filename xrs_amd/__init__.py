@@ -16,7 +16,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-__all__ = ["XRS", "XRSError", "lib", "LIB_PATH"]
+__all__ = ["XRS", "XRSError", "lib", "LIB_PATH", "batch_strides"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
@@ -58,6 +58,7 @@ def _load():
         "xrs_reconst": ([P, PP, I, Z, IP, I, IP, I], I),
         "xrs_update": ([P, P, P, Z, I, PP, I], I),
         "xrs_replace": ([P, PP, IP, I, Z, PP, I], I),
+        "xrs_batch_strides": ([Z, I, ctypes.POINTER(Z), ctypes.POINTER(Z)], I),
         "xrs_encode_batched": ([P, P, Z, Z, Z, Z, P], I),
         "xrs_reconst_one_batched": ([P, P, Z, Z, Z, Z, I, P], I),
         "xrs_reconst_batched": ([P, P, Z, Z, Z, Z, IP, I, IP, I, P], I),
@@ -99,6 +100,13 @@ def _ints(xs):
     for i, v in enumerate(xs):
         a[i] = int(v)
     return a
+
+
+def batch_strides(size: int, n_shards: int):
+    """Recommended (shard_stride, stripe_stride) for a device batch."""
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    _raise(_lib.xrs_batch_strides(size, n_shards, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def _raise(code: int, arg: int = 0):

@@ -558,6 +558,20 @@ int xrs_get_need_vects(const xrs_codec* x, int k, int* a_need, int* a_len, int b
 }
 
 // ---------------------------------------------------------------- batched
+// Pads measured with tools/kbench.hip (padab, interleaved medians, 4 GiB
+// batches): <= 64 KiB vects stream best back to back; 1 MiB vects lose 9% on
+// ReconstOne without a 256 B pad; 8 MiB vects lose 30% on Encode without a
+// 4 KiB + 256 B pad.
+int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* stripe_stride) {
+  if (!shard_stride || !stripe_stride || n_shards < 1) return XRS_ERR_INVALID_ARG;
+  size_t pad = 0;
+  if (size > (64u << 10)) pad = size >= (4u << 20) ? 4096 + 256 : 256;
+  const size_t s = (size + 15) / 16 * 16 + pad;
+  *shard_stride = s;
+  *stripe_stride = s * static_cast<size_t>(n_shards);
+  return XRS_OK;
+}
+
 int xrs_encode_batched(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
                        size_t stripe_stride, size_t n_stripes, void* stream) {
   if (!x) return XRS_ERR_INVALID_ARG;

@@ -31,6 +31,9 @@ constexpr int kDyn = -1;  // count known only at run time
 constexpr int kBlock = 256;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Global (address space 1) views: global_load/store instead of flat_*.
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+typedef __attribute__((address_space(1))) uint8_t gu8;
 
 __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c
@@ -52,18 +55,20 @@ __device__ __forceinline__ uint32_t gmul(const GfTab& t, const Sel& s) {
 }
 
 // ---- fragment load/store: W dwords per lane per row ------------------------
-// VEC: one 16-byte dwordx4 access (address 16-byte aligned).
+// VEC: one 16-byte dwordx4 access (address 16-byte aligned), nontemporal:
+// every shard byte is touched exactly once per launch (measured on MI355X:
+// nt loads + nt stores +3% Encode, +7..11% ReconstOne; tools/kbench.hip).
 // !VEC: nb (1..4) single-byte accesses (any alignment, ragged tail).
 template <bool VEC>
 __device__ __forceinline__ void ld(uint32_t* v, uint64_t addr, int nb) {
   if constexpr (VEC) {
-    const u32x4 t = *reinterpret_cast<const u32x4*>(addr);
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(addr));
     v[0] = t.x;
     v[1] = t.y;
     v[2] = t.z;
     v[3] = t.w;
   } else {
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(addr);
+    const gu8* p = reinterpret_cast<const gu8*>(addr);
     uint32_t x = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -80,9 +85,9 @@ __device__ __forceinline__ void st(const uint32_t* v, uint64_t addr, int nb) {
     t.y = v[1];
     t.z = v[2];
     t.w = v[3];
-    *reinterpret_cast<u32x4*>(addr) = t;
+    __builtin_nontemporal_store(t, reinterpret_cast<gu32x4*>(addr));
   } else {
-    uint8_t* p = reinterpret_cast<uint8_t*>(addr);
+    gu8* p = reinterpret_cast<gu8*>(addr);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (i < nb) p[i] = static_cast<uint8_t>(v[0] >> (8 * i));

@@ -123,6 +123,22 @@ int xrs_replace_batched(const xrs_codec *codec, const uint8_t *data_base,
                         int n, size_t size, uint8_t *parity_base, size_t parity_shard_stride,
                         size_t parity_stripe_stride, size_t n_stripes, void *stream);
 
+/* ---- host-resident batches (pipelined, synchronous) -------------------- *
+ * The real caller's path (shards start and end in host memory, e.g. disk or
+ * NIC buffers): stripes are moved in chunks through device slots on three
+ * streams so H2D, kernel and D2H overlap.  Host layout as for *_batched.
+ * Use pinned memory (xrs_host_alloc / xrs_host_register) for full PCIe rate;
+ * pageable memory works but copies synchronously. */
+int xrs_encode_host(const xrs_codec *codec, uint8_t *host_base, size_t size, size_t shard_stride,
+                    size_t stripe_stride, size_t n_stripes);
+/* ReconstOne(k) per stripe; only the GetNeedVects halves cross PCIe. */
+int xrs_reconst_one_host(const xrs_codec *codec, uint8_t *host_base, size_t size,
+                         size_t shard_stride, size_t stripe_stride, size_t n_stripes, int k);
+void *xrs_host_alloc(size_t bytes);           /* pinned host memory (NULL on failure) */
+void xrs_host_free(void *p);
+int xrs_host_register(void *p, size_t bytes); /* pin existing host memory */
+int xrs_host_unregister(void *p);
+
 #ifdef __cplusplus
 }
 #endif

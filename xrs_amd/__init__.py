@@ -64,6 +64,12 @@ def _load():
         "xrs_reconst_batched": ([P, P, Z, Z, Z, Z, IP, I, IP, I, P], I),
         "xrs_update_batched": ([P, P, Z, P, Z, Z, I, P, Z, Z, Z, P], I),
         "xrs_replace_batched": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z, P], I),
+        "xrs_encode_host": ([P, P, Z, Z, Z, Z], I),
+        "xrs_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
+        "xrs_host_alloc": ([Z], P),
+        "xrs_host_free": ([P], None),
+        "xrs_host_register": ([P, Z], I),
+        "xrs_host_unregister": ([P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -196,6 +202,19 @@ class XRS:
                               _ptrs(parity), len(parity))
         bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
+
+    # ------------------------------------------- host-resident pipelined API
+    # host_base: address of a host buffer (pinned for full PCIe rate).
+    def encode_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                    n_stripes: int) -> None:
+        _raise(_lib.xrs_encode_host(self._h, host_base, size, shard_stride, stripe_stride,
+                                    n_stripes), size)
+
+    def reconst_one_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                         n_stripes: int, k: int) -> None:
+        rc = _lib.xrs_reconst_one_host(self._h, host_base, size, shard_stride, stripe_stride,
+                                       n_stripes, int(k))
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else k)
 
     # ------------------------------------------- batched device-resident API
     # Pointers are device addresses (int); stream is a hipStream_t as int (0 = null).

@@ -40,6 +40,15 @@ struct xrs_codec {
   mutable size_t staging_cap = 0;
   mutable hipStream_t stream = nullptr;
 
+  // host-resident pipeline state (lazy; guarded by pipe_mu): kPipe device
+  // slots, one stream each, so chunk i+1's H2D, chunk i's kernel and chunk
+  // i-1's D2H overlap.
+  static constexpr int kPipe = 3;
+  mutable std::mutex pipe_mu;
+  mutable uint8_t* slot[kPipe] = {nullptr, nullptr, nullptr};
+  mutable size_t slot_cap = 0;
+  mutable hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
+
   uint8_t g(int row, int col) const { return gen[static_cast<size_t>(row) * d + col]; }
 };
 
@@ -434,6 +443,91 @@ int d2h(const xrs_codec* x, void* dst, size_t off, size_t n) {
 }
 int sync(const xrs_codec* x) { return hip_err(hipStreamSynchronize(x->stream)); }
 
+// ---------------------------------------------------- host-resident pipeline
+constexpr size_t kChunkBytes = 64u << 20;  // device bytes per pipeline chunk
+
+int ensure_pipe(const xrs_codec* x, size_t bytes) {
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  for (int i = 0; i < xrs_codec::kPipe; ++i)
+    if (!x->pstream[i] && hipStreamCreateWithFlags(&x->pstream[i], hipStreamNonBlocking) != hipSuccess)
+      return XRS_ERR_HIP;
+  if (bytes > x->slot_cap) {
+    for (int i = 0; i < xrs_codec::kPipe; ++i) {
+      if (x->slot[i]) (void)hipFree(x->slot[i]);
+      x->slot[i] = nullptr;
+    }
+    x->slot_cap = 0;
+    for (int i = 0; i < xrs_codec::kPipe; ++i)
+      if (hipMalloc(&x->slot[i], bytes) != hipSuccess) return XRS_ERR_HIP;
+    x->slot_cap = bytes;
+  }
+  return XRS_OK;
+}
+
+// One strided row copy for a chunk: `rows` stripes, `width` bytes each.
+int copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+           hipMemcpyKind kind, hipStream_t s) {
+  if (width == 0 || rows == 0) return XRS_OK;
+  return hip_err(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s));
+}
+
+struct HostBatch {
+  uint8_t* base;
+  size_t size, shard_stride, stripe_stride, n_stripes;
+  uint8_t* row(size_t stripe, int shard, size_t off) const {
+    return base + stripe * stripe_stride + static_cast<size_t>(shard) * shard_stride + off;
+  }
+};
+
+// Chunked H2D -> kernel -> D2H over kPipe streams.  `in` / `out` list the
+// (shard, half) pieces moved per stripe (half: 0 = a, 1 = b, 2 = whole vect);
+// `launch(slot_base, n, stream)` runs the op on the compact device layout.
+template <class Launch>
+int run_pipeline(const xrs_codec* x, const HostBatch& hb,
+                 const std::vector<std::pair<int, int>>& in,
+                 const std::vector<std::pair<int, int>>& out, Launch launch) {
+  const int nshards = x->d + x->p;
+  const size_t S = hb.size, H = S / 2;
+  const size_t dev_stripe = static_cast<size_t>(nshards) * S;
+  const size_t chunk = std::max<size_t>(1, std::min(hb.n_stripes, kChunkBytes / dev_stripe));
+  std::lock_guard<std::mutex> lk(x->pipe_mu);
+  DeviceGuard g(x->device);
+  int e = ensure_pipe(x, chunk * dev_stripe);
+  if (e) return e;
+  auto piece = [&](int half, size_t* off, size_t* len) {
+    *off = half == 1 ? H : 0;
+    *len = half == 2 ? S : H;
+  };
+  size_t i = 0;
+  for (size_t c0 = 0; c0 < hb.n_stripes && !e; c0 += chunk, ++i) {
+    const int si = static_cast<int>(i % xrs_codec::kPipe);
+    hipStream_t st = x->pstream[si];
+    uint8_t* slot = x->slot[si];
+    const size_t nc = std::min(chunk, hb.n_stripes - c0);
+    for (auto& p : in) {
+      size_t off, len;
+      piece(p.second, &off, &len);
+      if ((e = copy2d(slot + static_cast<size_t>(p.first) * S + off, dev_stripe,
+                      hb.row(c0, p.first, off), hb.stripe_stride, len, nc,
+                      hipMemcpyHostToDevice, st)))
+        break;
+    }
+    if (!e) e = launch(slot, nc, st);
+    for (auto& p : out) {
+      if (e) break;
+      size_t off, len;
+      piece(p.second, &off, &len);
+      e = copy2d(hb.row(c0, p.first, off), hb.stripe_stride,
+                 slot + static_cast<size_t>(p.first) * S + off, dev_stripe, len, nc,
+                 hipMemcpyDeviceToHost, st);
+    }
+  }
+  int es = XRS_OK;
+  for (int k = 0; k < xrs_codec::kPipe; ++k)
+    if (hipStreamSynchronize(x->pstream[k]) != hipSuccess) es = XRS_ERR_HIP;
+  return e ? e : es;
+}
+
 bool vects_ok(uint8_t* const* v, int n) {
   if (!v) return false;
   for (int i = 0; i < n; ++i)
@@ -514,10 +608,14 @@ int xrs_new(int data_num, int parity_num, xrs_codec** out) {
 
 void xrs_free(xrs_codec* x) {
   if (!x) return;
-  if (x->device >= 0 && (x->stream || x->staging)) {
+  if (x->device >= 0) {
     DeviceGuard g(x->device);
     if (x->stream) (void)hipStreamDestroy(x->stream);
     if (x->staging) (void)hipFree(x->staging);
+    for (int i = 0; i < xrs_codec::kPipe; ++i) {
+      if (x->pstream[i]) (void)hipStreamDestroy(x->pstream[i]);
+      if (x->slot[i]) (void)hipFree(x->slot[i]);
+    }
   }
   delete x;
 }
@@ -644,6 +742,67 @@ int xrs_replace_batched(const xrs_codec* x, const uint8_t* data_base, size_t dat
   return replace_impl(x, {const_cast<uint8_t*>(data_base), data_shard_stride, data_stripe_stride},
                       rows, n, size, {parity_base, parity_shard_stride, parity_stripe_stride},
                       n_stripes, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------ host-resident batches
+int xrs_encode_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t shard_stride,
+                    size_t stripe_stride, size_t n_stripes) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!host_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const int d = x->d, p = x->p;
+  std::vector<std::pair<int, int>> in, out;
+  for (int j = 0; j < d; ++j) in.push_back({j, 2});
+  for (int r = 0; r < p; ++r) out.push_back({d + r, 2});
+  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
+  const size_t dev_stripe = static_cast<size_t>(d + p) * size;
+  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return encode_impl(x, {slot, size, dev_stripe}, size, n, s);
+  });
+}
+
+int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t shard_stride,
+                         size_t stripe_stride, size_t n_stripes, int k) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  std::vector<int> a_need;
+  int bi = 0;
+  if ((e = need_vects(x, k, &a_need, &bi))) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!host_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const int d = x->d, p = x->p;
+  // Only the GetNeedVects set crosses PCIe (xrs.go:146-171).
+  std::vector<std::pair<int, int>> in, out = {{k, 2}};
+  for (int m = 0; m < d; ++m) in.push_back({m == k ? d : m, 1});
+  in.push_back({bi, 1});
+  for (int i : a_need) in.push_back({i, 0});
+  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
+  const size_t dev_stripe = static_cast<size_t>(d + p) * size;
+  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return reconst_one_impl(x, {slot, size, dev_stripe}, size, n, k, s);
+  });
+}
+
+void* xrs_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+void xrs_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+int xrs_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return XRS_ERR_INVALID_ARG;
+  return hip_err(hipHostRegister(p, bytes, hipHostRegisterDefault));
+}
+int xrs_host_unregister(void* p) {
+  if (!p) return XRS_ERR_INVALID_ARG;
+  return hip_err(hipHostUnregister(p));
 }
 
 // ------------------------------------------------------------------- sync

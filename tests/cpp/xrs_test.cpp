@@ -1,0 +1,266 @@
+// xrs_test.cpp -- the reference's test file (/root/reference/xrs_test.go)
+// ported to C++ over include/xrs.hpp (the C++ mirror of the Go method set).
+// Fixed seeds instead of the reference's clock seeds (xrs_test.go:26-31).
+//
+//   xrs_test --cpu   host-logic tests only (no GPU needed)
+//   xrs_test         all tests (needs the MI355X)
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+
+#include "xrs.hpp"
+
+using xrs::Error;
+using xrs::Vect;
+using xrs::Vects;
+using xrs::XRS;
+
+static int g_fail = 0;
+#define FATAL(...)                          \
+  do {                                      \
+    std::printf("FAIL %s: ", __func__);     \
+    std::printf(__VA_ARGS__);               \
+    std::printf("\n");                      \
+    ++g_fail;                               \
+    return;                                 \
+  } while (0)
+
+static const int kData = 12, kParity = 4, kShard = 1024;  // xrs_test.go:21-23
+
+static Vects new_shard_matrix(int shards, int size) { return Vects(shards, Vect(size, 0)); }
+static void fill_random(std::mt19937_64& r, Vect& v) {
+  for (auto& b : v) b = static_cast<uint8_t>(r());
+}
+static bool is_in(int e, const std::vector<int>& s) {
+  return std::find(s.begin(), s.end(), e) != s.end();
+}
+static std::unique_ptr<XRS> must_new(int d, int p) {
+  std::unique_ptr<XRS> x;
+  if (Error e = XRS::New(d, p, &x)) {
+    std::printf("New(%d,%d): %s\n", d, p, e.msg.c_str());
+    std::exit(2);
+  }
+  return x;
+}
+
+// xrs_test.go:83-99 makeXORSetOld
+static std::map<int, std::vector<int>> make_xorset_old(int d, int p) {
+  std::map<int, std::vector<int>> m;
+  int a = 0;
+  for (;;) {
+    if (a == d) break;
+    for (int i = d + 1; i < d + p; ++i) {
+      if (a == d) break;
+      m[i].push_back(a);
+      ++a;
+    }
+  }
+  return m;
+}
+
+// xrs_test.go:51-80
+static void TestMakeXORSet() {
+  for (int d = 1; d <= 255; ++d)
+    for (int p = 2; p <= 255; ++p) {
+      if (d + p > 256) continue;
+      auto x = must_new(d, p);
+      if (x->XORSet() != make_xorset_old(d, p)) FATAL("mismatch %d+%d", d, p);
+    }
+}
+
+// xrs_test.go:124-156
+static void TestXRS_GetNeedVects() {
+  for (int d = 1; d <= 255; ++d)
+    for (int p = 2; p <= 255; ++p) {
+      if (d + p > 256) continue;
+      auto x = must_new(d, p);
+      for (int i = 0; i < d; ++i) {
+        std::vector<int> a, b;
+        if (Error e = x->GetNeedVects(i, &a, &b)) FATAL("%s", e.msg.c_str());
+        a.push_back(i);
+        std::sort(a.begin(), a.end());
+        if (a != x->XORSet().at(b[1])) FATAL("element mismatch %d+%d i=%d", d, p, i);
+      }
+    }
+}
+
+static void TestErrors() {
+  std::unique_ptr<XRS> x;
+  Error e = XRS::New(10, 1, &x);
+  if (e.msg != "illegal parity") FATAL("got '%s'", e.msg.c_str());
+  x = must_new(kData, kParity);
+  std::vector<int> a, b;
+  e = x->GetNeedVects(12, &a, &b);
+  if (e.msg != "illegal data index: 12") FATAL("got '%s'", e.msg.c_str());
+  Vects odd = new_shard_matrix(kData + kParity, 3);
+  e = x->Encode(odd);
+  if (e.msg != "vect size not even: 3") FATAL("got '%s'", e.msg.c_str());
+}
+
+// xrs_test.go:101-122 ("Powered by MATLAB")
+static void TestXRS_Encode() {
+  auto x = must_new(5, 5);
+  Vects vects = {{0, 0}, {4, 7}, {2, 4}, {6, 9}, {8, 11}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  if (Error e = x->Encode(vects)) FATAL("%s", e.msg.c_str());
+  Vects exp = {{0, 0}, {4, 7}, {2, 4}, {6, 9}, {8, 11}, {97, 156}, {173, 117}, {218, 110},
+               {107, 59}, {110, 153}};
+  for (size_t i = 0; i < exp.size(); ++i)
+    if (vects[i] != exp[i]) FATAL("encode failed: vect %zu mismatch", i);
+}
+
+// xrs_test.go:162-227 testReconstOne
+static void testReconstOne(int data, int parity, int size) {
+  std::mt19937_64 r(1);
+  for (int lost = 0; lost < data; ++lost) {
+    Vects expect = new_shard_matrix(data + parity, size);
+    for (int j = 0; j < data; ++j) fill_random(r, expect[j]);
+    auto x = must_new(data, parity);
+    if (Error e = x->Encode(expect)) FATAL("%s", e.msg.c_str());
+    Vects result = expect;
+    result[lost].assign(size, 0);
+    std::vector<int> a_need, b_need;
+    if (Error e = x->GetNeedVects(lost, &a_need, &b_need)) FATAL("%s", e.msg.c_str());
+    const int half = size / 2;
+    for (int j = 0; j < data + parity; ++j) {
+      if (!is_in(j, a_need)) std::fill(result[j].begin(), result[j].begin() + half, 0);
+      if (j >= data && !is_in(j, b_need)) std::fill(result[j].begin() + half, result[j].end(), 0);
+    }
+    std::fill(result[lost].begin() + half, result[lost].end(), 0);
+    if (Error e = x->ReconstOne(result, lost)) FATAL("%s", e.msg.c_str());
+    if (result[lost] != expect[lost]) FATAL("mismatch reconstOne; vect: %d; size: %d", lost, size);
+  }
+}
+static void TestXRS_ReconstOne() {
+  testReconstOne(kData, kParity, 2);  // xrs_test.go:159
+  testReconstOne(kData, kParity, 4096);
+}
+
+static std::vector<int> make_lost_random(std::mt19937_64& r, int n, int lost_n) {
+  std::vector<int> l;
+  while (static_cast<int>(l.size()) < lost_n) {
+    int v = static_cast<int>(r() % n);
+    if (!is_in(v, l)) l.push_back(v);
+  }
+  return l;
+}
+static std::vector<int> make_has_from_lost(int n, const std::vector<int>& lost) {
+  std::vector<int> s;
+  for (int i = 0; i < n; ++i)
+    if (!is_in(i, lost)) s.push_back(i);
+  return s;
+}
+
+// xrs_test.go:265-314 testReconst
+static void testReconst(int data, int parity, int size, int loop) {
+  std::mt19937_64 r(2);
+  auto x = must_new(data, parity);
+  for (int i = 0; i < loop; ++i) {
+    Vects exp = new_shard_matrix(data + parity, size), act = new_shard_matrix(data + parity, size);
+    for (int j = 0; j < data; ++j) fill_random(r, exp[j]);
+    if (Error e = x->Encode(exp)) FATAL("%s", e.msg.c_str());
+    std::vector<int> lost = make_lost_random(r, data + parity, static_cast<int>(r() % (parity + 1)));
+    std::vector<int> need(lost.begin(), lost.begin() + r() % (lost.size() + 1));
+    if (need.size() == 1) lost = need;
+    std::vector<int> has = make_has_from_lost(data + parity, lost);
+    for (int h : has) act[h] = exp[h];
+    for (int nr : need)
+      if (r() % 4 == 0) act[nr] = exp[nr];
+    if (Error e = x->Reconst(act, has, need)) FATAL("%s", e.msg.c_str());
+    for (int n : need)
+      if (exp[n] != act[n]) FATAL("reconst failed: vect: %d, size: %d", n, size);
+  }
+}
+static void TestXRS_Reconst() { testReconst(kData, kParity, kShard, 128); }
+
+// xrs_test.go:320-359 testUpdate
+static void testUpdate(int data, int parity, int size) {
+  std::mt19937_64 r(3);
+  auto x = must_new(data, parity);
+  for (int i = 0; i < data; ++i) {
+    Vects act = new_shard_matrix(data + parity, size), exp = new_shard_matrix(data + parity, size);
+    for (int j = 0; j < data; ++j) {
+      fill_random(r, exp[j]);
+      act[j] = exp[j];
+    }
+    if (Error e = x->Encode(act)) FATAL("%s", e.msg.c_str());
+    Vect nd(size);
+    fill_random(r, nd);
+    if (Error e = x->Update(act[i], nd, i, xrs::slices(act, data))) FATAL("%s", e.msg.c_str());
+    exp[i] = nd;
+    if (Error e = x->Encode(exp)) FATAL("%s", e.msg.c_str());
+    for (int j = data; j < data + parity; ++j)
+      if (act[j] != exp[j]) FATAL("update failed: vect: %d, size: %d", j, size);
+  }
+}
+static void TestXRS_Update() { testUpdate(kData, kParity, kShard); }
+
+// xrs_test.go:423-441
+static std::vector<int> make_replace_rows_random(std::mt19937_64& r, int data) {
+  const int n = static_cast<int>(r() % (data + 1));
+  std::vector<int> s;
+  for (int i = 0; i < 64 && static_cast<int>(s.size()) < n; ++i) {
+    int v = static_cast<int>(r() % data);
+    if (!is_in(v, s)) s.push_back(v);
+  }
+  if (s.empty()) s.push_back(0);
+  return s;
+}
+
+// xrs_test.go:366-421 testReplace
+static void testReplace(int data, int parity, int size, int loop, bool to_zero) {
+  std::mt19937_64 r(to_zero ? 4 : 5);
+  auto x = must_new(data, parity);
+  for (int i = 0; i < loop; ++i) {
+    std::vector<int> rows = make_replace_rows_random(r, data);
+    Vects act = new_shard_matrix(data + parity, size), exp = new_shard_matrix(data + parity, size);
+    for (int j = 0; j < data; ++j) {
+      fill_random(r, exp[j]);
+      act[j] = exp[j];
+    }
+    Vects dv;
+    for (int rr : rows) dv.push_back(exp[rr]);
+    if (to_zero)
+      for (int rr : rows) exp[rr].assign(size, 0);
+    if (Error e = x->Encode(exp)) FATAL("%s", e.msg.c_str());
+    if (!to_zero)
+      for (int rr : rows) act[rr].assign(size, 0);
+    if (Error e = x->Encode(act)) FATAL("%s", e.msg.c_str());
+    if (Error e = x->Replace(xrs::slices(dv), rows, xrs::slices(act, data)))
+      FATAL("%s", e.msg.c_str());
+    for (int j = data; j < data + parity; ++j)
+      if (act[j] != exp[j]) FATAL("replace failed: vect: %d, size: %d", j, size);
+  }
+}
+static void TestXRS_Replace() {
+  testReplace(kData, kParity, kShard, 1024, true);
+  testReplace(kData, kParity, kShard, 1024, false);
+}
+
+int main(int argc, char** argv) {
+  const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
+  struct T {
+    const char* name;
+    void (*fn)();
+    bool gpu;
+  } tests[] = {
+      {"TestMakeXORSet", TestMakeXORSet, false},
+      {"TestXRS_GetNeedVects", TestXRS_GetNeedVects, false},
+      {"TestErrors", TestErrors, false},
+      {"TestXRS_Encode", TestXRS_Encode, true},
+      {"TestXRS_ReconstOne", TestXRS_ReconstOne, true},
+      {"TestXRS_Reconst", TestXRS_Reconst, true},
+      {"TestXRS_Update", TestXRS_Update, true},
+      {"TestXRS_Replace", TestXRS_Replace, true},
+  };
+  for (const T& t : tests) {
+    if (cpu_only && t.gpu) continue;
+    const int before = g_fail;
+    t.fn();
+    std::printf("%s %s\n", g_fail == before ? "ok  " : "FAIL", t.name);
+  }
+  std::printf("%s\n", g_fail ? "FAIL" : "PASS");
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,29 @@
+"""Runs the C++ port of the reference's tests (tests/cpp/xrs_test.cpp, over
+include/xrs.hpp): host-logic tests on CPU, all tests on the GPU box."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "xrs_test")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+
+
+def test_cpp_host_logic():
+    build()
+    r = subprocess.run([BIN, "--cpu"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_all_on_gpu():
+    if not os.path.exists(BIN):
+        build()
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout

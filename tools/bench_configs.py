@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Device-resident throughput of every BASELINE.json config on one MI355X
+(the driver's bench.py line covers the headline; this fills DESIGN.md).
+
+Byte accounting = the reference's SetBytes (xrs_test.go:513, :565-572, :622,
+:672): Encode (d+p)*S, ReconstOne 9*S, Reconst(n lost data) (d+n)*S,
+Update (2p+2)*S, Replace(n) (n+2p)*S per stripe.  One JSON line per case.
+"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import xrs_amd  # noqa: E402
+
+D, P = 12, 4
+PEAK = 8.0e12
+
+
+def timed(fn, reps=10, warm=2):
+    for i in range(warm):
+        fn(i)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for i in range(reps):
+        fn(i)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+def emit(name, size, n, secs, nbytes, shard):
+    print(json.dumps({"case": name, "vect_bytes": size, "stripes": n, "shard_stride": shard,
+                      "ms": round(secs * 1e3, 4), "gibps": round(nbytes / secs / 2**30, 1),
+                      "gbs": round(nbytes / secs / 1e9, 1),
+                      "frac_of_8TBs": round(nbytes / secs / PEAK, 4)}), flush=True)
+
+
+def batch(size, n, dev, seed, padded=True):
+    shard, stripe = xrs_amd.batch_strides(size, D + P) if padded else (size, (D + P) * size)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    t = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device=dev, generator=g)
+    return t, shard, stripe
+
+
+def main():
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    x = xrs_amd.XRS(D, P)
+    cases = sys.argv[1:] or ["c2", "c3", "c4", "c5", "multi"]
+    if "c2" in cases:  # 12+4 Encode @ 4 KiB
+        for padded in (True, False):
+            t, sh, st = batch(4096, 65536, dev, 1, padded)
+            secs = timed(lambda i: x.encode_batched(t.data_ptr(), 4096, sh, st, 65536, s))
+            emit("encode", 4096, 65536, secs, 65536 * 16 * 4096, sh)
+            del t
+    if "c3" in cases:  # ReconstOne @ 1 MiB
+        for padded in (True, False):
+            t, sh, st = batch(1 << 20, 512, dev, 2, padded)
+            x.encode_batched(t.data_ptr(), 1 << 20, sh, st, 512, s)
+            secs = timed(lambda i: x.reconst_one_batched(t.data_ptr(), 1 << 20, sh, st, 512, i % D, s))
+            emit("reconst_one", 1 << 20, 512, secs, 512 * 9 * (1 << 20), sh)
+            del t
+    if "c4" in cases:  # Update + Replace(4) @ 8 MiB
+        size, n = 8 << 20, 32
+        t, sh, st = batch(size, n, dev, 3)
+        x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+        new = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=dev)
+        par = t.data_ptr() + D * sh
+        secs = timed(lambda i: x.update_batched(t.data_ptr() + (i % D) * sh, st, new.data_ptr(),
+                                                size, size, i % D, par, sh, st, n, s))
+        emit("update", size, n, secs, n * (2 * P + 2) * size, sh)
+        for nrep in (1, 4, 8):
+            rows = list(range(nrep))
+            secs = timed(lambda i: x.replace_batched(t.data_ptr(), sh, st, rows, size, par, sh, st,
+                                                     n, s))
+            emit(f"replace_{nrep}", size, n, secs, n * (nrep + 2 * P) * size, sh)
+        del t, new
+    if "c5" in cases:  # 1 MiB, 8192 stripes per GPU (the 64k-stripe / 8-GPU split)
+        size, n = 1 << 20, 8192
+        t, sh, st = batch(size, n, dev, 4)
+        secs = timed(lambda i: x.encode_batched(t.data_ptr(), size, sh, st, n, s), reps=5, warm=1)
+        emit("encode", size, n, secs, n * 16 * size, sh)
+        secs = timed(lambda i: x.reconst_one_batched(t.data_ptr(), size, sh, st, n, i % D, s),
+                     reps=5, warm=1)
+        emit("reconst_one", size, n, secs, n * 9 * size, sh)
+        del t
+    if "multi" in cases:  # Reconst with 2..4 lost data vects (xrs_test.go:530-582)
+        for size, n in ((4096, 65536), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            for lost in (2, 3, 4):
+                need = list(range(lost))
+                has = list(range(lost, D + P))
+                secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has, need, s))
+                emit(f"reconst_{lost}", size, n, secs, n * (D + lost) * size, sh)
+            del t
+    torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,6 +143,149 @@ __global__ __launch_bounds__(256) void r1_skew(const RowsArgs<2, 12, 4, true> a)
   __builtin_nontemporal_store(s1 ^ s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[1], stripe, c * 16)));
 }
 
+// Encode variant with w-outer loops (table dwords for a column pair held in
+// VGPRs, selectors computed per dword) and optional dwordx2 lanes (VB = 8).
+template <int VB>
+__global__ __launch_bounds__(256) void enc_wouter(const PairArgs<4, 12, true> a) {
+  constexpr int P = 4, C = 12, W = VB / 4;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t chunks = a.half / VB;
+  if (gid >= chunks * (a.total / a.chunks)) return;
+  const uint64_t stripe = gid / chunks;
+  const uint64_t off = (gid - stripe * chunks) * VB;
+  uint32_t xa[C][W], xb[C][W];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const uint64_t s = row_addr(a.src[c], stripe, off);
+    if constexpr (VB == 16) {
+      u32x4 ta = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s));
+      u32x4 tb = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s + a.half));
+      xa[c][0] = ta.x; xa[c][1] = ta.y; xa[c][2] = ta.z; xa[c][3] = ta.w;
+      xb[c][0] = tb.x; xb[c][1] = tb.y; xb[c][2] = tb.z; xb[c][3] = tb.w;
+    } else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      typedef __attribute__((address_space(1))) u32x2 gu32x2;
+      u32x2 ta = __builtin_nontemporal_load(reinterpret_cast<const gu32x2*>(s));
+      u32x2 tb = __builtin_nontemporal_load(reinterpret_cast<const gu32x2*>(s + a.half));
+      xa[c][0] = ta.x; xa[c][1] = ta.y;
+      xb[c][0] = tb.x; xb[c][1] = tb.y;
+    }
+  }
+  uint32_t acc_a[P][W] = {}, acc_b[P][W] = {};
+#pragma unroll
+  for (int c = 0; c < C; c += 2) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const Sel sa0 = sel_of(xa[c][w]), sb0 = sel_of(xb[c][w]);
+      const Sel sa1 = sel_of(xa[c + 1][w]), sb1 = sel_of(xb[c + 1][w]);
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        acc_a[r][w] = x3(acc_a[r][w], gmul(a.tab[c][r], sa0), gmul(a.tab[c + 1][r], sa1));
+        acc_b[r][w] = x3(acc_b[r][w], gmul(a.tab[c][r], sb0), gmul(a.tab[c + 1][r], sb1));
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      acc_b[1 + c % 3][w] ^= xa[c][w];
+      acc_b[1 + (c + 1) % 3][w] ^= xa[c + 1][w];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const uint64_t d = row_addr(a.dst[r], stripe, off);
+    if constexpr (VB == 16) {
+      u32x4 ta, tb;
+      ta.x = acc_a[r][0]; ta.y = acc_a[r][1]; ta.z = acc_a[r][2]; ta.w = acc_a[r][3];
+      tb.x = acc_b[r][0]; tb.y = acc_b[r][1]; tb.z = acc_b[r][2]; tb.w = acc_b[r][3];
+      __builtin_nontemporal_store(ta, reinterpret_cast<gu32x4*>(d));
+      __builtin_nontemporal_store(tb, reinterpret_cast<gu32x4*>(d + a.half));
+    } else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      typedef __attribute__((address_space(1))) u32x2 gu32x2;
+      u32x2 ta, tb;
+      ta.x = acc_a[r][0]; ta.y = acc_a[r][1];
+      tb.x = acc_b[r][0]; tb.y = acc_b[r][1];
+      __builtin_nontemporal_store(ta, reinterpret_cast<gu32x2*>(d));
+      __builtin_nontemporal_store(tb, reinterpret_cast<gu32x2*>(d + a.half));
+    }
+  }
+}
+
+// Grid-stride XOR-only probes (memory ceiling with a persistent-style grid).
+__global__ __launch_bounds__(256) void r1_xor_gs(const RowsArgs<2, 12, 4, true> a) {
+  for (uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; gid < a.total;
+       gid += static_cast<uint64_t>(gridDim.x) * 256) {
+    const uint64_t stripe = gid / a.chunks;
+    const uint64_t off = (gid - stripe * a.chunks) * 16;
+    u32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 12; ++m)
+      s0 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.msrc[m], stripe, off)));
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      s1 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.xsrc[x], stripe, off)));
+    __builtin_nontemporal_store(s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[0], stripe, off)));
+    __builtin_nontemporal_store(s1 ^ s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[1], stripe, off)));
+  }
+}
+
+__global__ __launch_bounds__(256) void r1_xor_nt(const RowsArgs<2, 12, 4, true> a) {
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  u32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int m = 0; m < 12; ++m)
+    s0 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.msrc[m], stripe, off)));
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+    s1 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.xsrc[x], stripe, off)));
+  __builtin_nontemporal_store(s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[0], stripe, off)));
+  __builtin_nontemporal_store(s1 ^ s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[1], stripe, off)));
+}
+
+__global__ __launch_bounds__(256) void enc_xor_gs(const PairArgs<4, 12, true> a) {
+  for (uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; gid < a.total;
+       gid += static_cast<uint64_t>(gridDim.x) * 256) {
+    const uint64_t stripe = gid / a.chunks;
+    const uint64_t off = (gid - stripe * a.chunks) * 16;
+    u32x4 sa = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      const uint64_t s = row_addr(a.src[c], stripe, off);
+      sa ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s));
+      sb ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s + a.half));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t d = row_addr(a.dst[r], stripe, off);
+      __builtin_nontemporal_store(sa + r, reinterpret_cast<gu32x4*>(d));
+      __builtin_nontemporal_store(sb + r, reinterpret_cast<gu32x4*>(d + a.half));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void enc_xor_nt(const PairArgs<4, 12, true> a) {
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  u32x4 sa = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 12; ++c) {
+    const uint64_t s = row_addr(a.src[c], stripe, off);
+    sa ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s));
+    sb ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s + a.half));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t d = row_addr(a.dst[r], stripe, off);
+    __builtin_nontemporal_store(sa + r, reinterpret_cast<gu32x4*>(d));
+    __builtin_nontemporal_store(sb + r, reinterpret_cast<gu32x4*>(d + a.half));
+  }
+}
+
 // Same addresses, XOR only (memory ceiling of the ReconstOne pattern).
 __global__ __launch_bounds__(256) void r1_xoronly(const RowsArgs<2, 12, 4, true> a) {
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
@@ -353,6 +496,98 @@ int main(int argc, char** argv) {
   const std::string which = argc > 1 ? argv[1] : "all";
   const GF& gf = GF::get();
   Timer tm;
+  if (which == "gs") {
+    // ReconstOne 1 MiB (pad 256) and Encode 4 KiB (pad 0), 4 GiB batches.
+    const uint64_t S1 = 1 << 20, n1 = 256, H1 = S1 / 2, sh1 = S1 + 256, st1 = 16 * sh1;
+    const uint64_t S2 = 4096, n2 = 65536, H2 = S2 / 2, st2 = 16 * S2;
+    uint8_t *b1, *b2;
+    CK(hipMalloc(&b1, n1 * st1));
+    CK(hipMalloc(&b2, n2 * st2));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)b1, n1 * st1 / 4, 5u);
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)b2, n2 * st2 / 4, 6u);
+    const uint64_t base1 = reinterpret_cast<uint64_t>(b1), base2 = reinterpret_cast<uint64_t>(b2);
+    RowsArgs<2, 12, 4, true> ra;
+    std::memset(&ra, 0, sizeof(ra));
+    for (int m = 0; m < 12; ++m) {
+      ra.msrc[m] = {base1 + (m == 0 ? 12 : m) * sh1 + H1, st1};
+      for (int r = 0; r < 2; ++r) ra.tab[m][r] = gf.tab(static_cast<uint8_t>(17 * m + 5 * r + 3));
+    }
+    ra.xsrc[0] = {base1 + 13 * sh1 + H1, st1};
+    for (int x = 1; x < 4; ++x) ra.xsrc[x] = {base1 + 3 * x * sh1, st1};
+    for (int x = 0; x < 4; ++x) ra.xmask[x] = 2;
+    ra.dst[0] = {base1 + H1, st1};
+    ra.dst[1] = {base1, st1};
+    ra.nm = 12; ra.nx = 4; ra.len = H1; ra.chunks = H1 / 16; ra.total = ra.chunks * n1;
+    PairArgs<4, 12, true> pa;
+    std::memset(&pa, 0, sizeof(pa));
+    for (int c = 0; c < 12; ++c) {
+      pa.src[c] = {base2 + c * S2, st2};
+      for (int r = 0; r < 4; ++r) pa.tab[c][r] = gf.tab(gf.inv(static_cast<uint8_t>((12 + r) ^ c)));
+    }
+    for (int r = 0; r < 4; ++r) pa.dst[r] = {base2 + (12 + r) * S2, st2};
+    pa.n_src = 12; pa.half = H2; pa.chunks = H2 / 16; pa.total = pa.chunks * n2;
+    const unsigned bl1 = (unsigned)(ra.total / 256), bl2 = (unsigned)(pa.total / 256);
+    const unsigned grids[] = {1024, 2048, 4096, 8192, 16384};
+    std::vector<double> tr[8], te[8];
+    for (int round = 0; round < 7; ++round) {
+      tr[0].push_back(tm.ms([&] { hipLaunchKernelGGL((rows_kernel<2, 12, 4, false, true>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+      tr[1].push_back(tm.ms([&] { hipLaunchKernelGGL(r1_xor_nt, dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+      te[0].push_back(tm.ms([&] { hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+      te[1].push_back(tm.ms([&] { hipLaunchKernelGGL(enc_xor_nt, dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+      for (int g = 0; g < 5; ++g) {
+        tr[2 + g].push_back(tm.ms([&] { hipLaunchKernelGGL(r1_xor_gs, dim3(grids[g]), dim3(256), 0, 0, ra); }, 5));
+        te[2 + g].push_back(tm.ms([&] { hipLaunchKernelGGL(enc_xor_gs, dim3(grids[g]), dim3(256), 0, 0, pa); }, 5));
+      }
+    }
+    for (int i = 0; i < 7; ++i) {
+      std::sort(tr[i].begin(), tr[i].end());
+      std::sort(te[i].begin(), te[i].end());
+      char name[128];
+      if (i < 2) std::snprintf(name, sizeof name, "r1 1MiB pad256 %s", i ? "xor-only nt" : "product");
+      else std::snprintf(name, sizeof name, "r1 1MiB pad256 xor grid-stride g=%u", grids[i - 2]);
+      report(name, tr[i][3], 9.0 * S1 * n1);
+      if (i < 2) std::snprintf(name, sizeof name, "enc 4KiB %s", i ? "xor-only nt" : "product");
+      else std::snprintf(name, sizeof name, "enc 4KiB xor grid-stride g=%u", grids[i - 2]);
+      report(name, te[i][3], 16.0 * S2 * n2);
+    }
+    return 0;
+  }
+  if (which == "encvar") {
+    const uint64_t S2 = 4096, n2 = 65536, H2 = S2 / 2, st2 = 16 * S2;
+    uint8_t* b2;
+    CK(hipMalloc(&b2, n2 * st2));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)b2, n2 * st2 / 4, 6u);
+    const uint64_t base2 = reinterpret_cast<uint64_t>(b2);
+    PairArgs<4, 12, true> pa;
+    std::memset(&pa, 0, sizeof(pa));
+    for (int c = 0; c < 12; ++c) {
+      pa.src[c] = {base2 + c * S2, st2};
+      for (int r = 0; r < 4; ++r) pa.tab[c][r] = gf.tab(gf.inv(static_cast<uint8_t>((12 + r) ^ c)));
+    }
+    for (int r = 0; r < 4; ++r) pa.dst[r] = {base2 + (12 + r) * S2, st2};
+    pa.n_src = 12; pa.half = H2; pa.chunks = H2 / 16; pa.total = pa.chunks * n2;
+    const unsigned bl = (unsigned)(pa.total / 256);
+    hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl), dim3(256), 0, 0, pa);
+    const unsigned long long ref = checksum(b2, n2 * st2);
+    std::vector<double> t[4];
+    const char* nm[4] = {"product", "xor-only nt", "w-outer x4", "w-outer x2"};
+    for (int round = 0; round < 7; ++round) {
+      t[0].push_back(tm.ms([&] { hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl), dim3(256), 0, 0, pa); }, 5));
+      t[1].push_back(tm.ms([&] { hipLaunchKernelGGL(enc_xor_nt, dim3(bl), dim3(256), 0, 0, pa); }, 5));
+      hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl), dim3(256), 0, 0, pa);
+      t[2].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_wouter<16>), dim3(bl), dim3(256), 0, 0, pa); }, 5));
+      if (round == 0 && checksum(b2, n2 * st2) != ref) std::printf("   !! w-outer x4 differs\n");
+      t[3].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_wouter<8>), dim3(2 * bl), dim3(256), 0, 0, pa); }, 5));
+      if (round == 0 && checksum(b2, n2 * st2) != ref) std::printf("   !! w-outer x2 differs\n");
+    }
+    for (int i = 0; i < 4; ++i) {
+      std::sort(t[i].begin(), t[i].end());
+      char name[96];
+      std::snprintf(name, sizeof name, "enc 4KiB %s", nm[i]);
+      report(name, t[i][3], 16.0 * S2 * n2);
+    }
+    return 0;
+  }
   if (which == "skew") {
     const uint64_t S = 1 << 20, n = 256, H = S / 2;
     for (uint64_t pad : {0ull, 256ull}) {

@@ -1,0 +1,81 @@
+"""GPU edge cases of general Reconst (xrs.go:236-301) against the oracle:
+repeated indexes (the reference's loops apply an XOR once per occurrence),
+a need list holding survivors, losses with an empty need (side effects only),
+and error ordering."""
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleError, OracleXRS
+
+pytestmark = pytest.mark.gpu
+D, P = 12, 4
+
+
+def stripe(rng, size):
+    o = OracleXRS(D, P)
+    v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D)]
+    v += [np.zeros(size, np.uint8) for _ in range(P)]
+    o.encode(v)
+    return v
+
+
+CASES = [
+    (list(range(2, 16)) + [14, 15], [0, 1]),          # repeated survivors (parity, twice)
+    (list(range(2, 16)) + [13], [0, 1, 1]),            # repeated need
+    (list(range(1, 14)), [14, 14, 15, 0]),             # repeated parity need (re-piggyback x2)
+    ([i for i in range(16) if i not in (3, 13)], [3, 13, 5]),  # need holds a survivor (5)
+    ([i for i in range(16) if i not in (3, 13)], []),  # losses, nothing needed: side effects
+    (list(range(16)), [14]),                           # nothing lost, parity "needed"
+    (list(range(4, 16)), [0, 1, 2, 3]),                # exactly d survivors
+]
+
+
+@pytest.mark.parametrize("has,need", CASES)
+@pytest.mark.parametrize("size", [2, 4096, 1030])
+def test_reconst_edge_vs_oracle(rng, has, need, size):
+    v = stripe(rng, size)
+    for i in range(D + P):
+        if i not in has:
+            v[i][:] = 0x5A
+    a = [r.copy() for r in v]
+    b = [r.copy() for r in v]
+    xrs_amd.XRS(D, P).reconst(a, has, need)
+    OracleXRS(D, P).reconst(b, has, need)
+    for i in range(D + P):
+        assert np.array_equal(a[i], b[i]), i
+
+
+@pytest.mark.parametrize("has,need,msg", [
+    (list(range(11)), [12, 13], "too few survivors"),
+    (list(range(12)) + [16], [13, 14], "illegal index"),
+    ([0] * 12 + [12], [13, 14], "singular matrix"),
+    (list(range(16)), [-1], "illegal data index: -1"),
+])
+def test_reconst_errors_match_oracle(rng, has, need, msg):
+    v = stripe(rng, 64)
+    for i in range(D + P):
+        if i not in has:
+            v[i][:] = 0
+    a = [r.copy() for r in v]
+    b = [r.copy() for r in v]
+    with pytest.raises(xrs_amd.XRSError, match=msg):
+        xrs_amd.XRS(D, P).reconst(a, has, need)
+    with pytest.raises(OracleError):
+        OracleXRS(D, P).reconst(b, has, need)
+    for i in range(D + P):  # the same (possibly partial) side effects
+        assert np.array_equal(a[i], b[i]), i
+
+
+@pytest.mark.gpu
+def test_cpp_port_under_host_asan():
+    """The C++ port of xrs_test.go linked against an ASan/UBSan (host code
+    only) build of the library sources: no host memory errors on GPU paths."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "build", "xrs_test_asan")
+    if not os.path.exists(exe):
+        pytest.skip("ASan build not present (tools/build_asan.sh)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]

@@ -79,3 +79,54 @@ def test_cpp_port_under_host_asan():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=900,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.fixture(params=["fused", "stepwise"])
+def reconst_mode(request, monkeypatch):
+    if request.param == "stepwise":
+        monkeypatch.setenv("XRS_RECONST_STEPWISE", "1")
+    else:
+        monkeypatch.delenv("XRS_RECONST_STEPWISE", raising=False)
+    return request.param
+
+
+@pytest.mark.parametrize("size", [2, 4096, 1030])
+def test_reconst_random_both_paths(rng, reconst_mode, size):
+    """General Reconst through the fused one-pass plan and the step-by-step
+    plan: identical buffers (side effects included) to the oracle."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    for _ in range(60):
+        v = stripe(rng, size)
+        lost = [int(t) for t in rng.permutation(D + P)[: int(rng.integers(0, P + 1))]]
+        need = lost[: int(rng.integers(0, len(lost) + 1))]
+        if rng.integers(0, 5) == 0 and need:
+            need = need + [need[0]]  # a repeated need
+        has = [i for i in range(D + P) if i not in lost]
+        if rng.integers(0, 4) == 0:
+            has = list(rng.permutation(has))  # survivors in any order
+        for t in lost:
+            v[t][:] = rng.integers(0, 256, size=size, dtype=np.uint8)
+        a = [r.copy() for r in v]
+        b = [r.copy() for r in v]
+        x.reconst(a, has, need)
+        o.reconst(b, has, need)
+        for i in range(D + P):
+            assert np.array_equal(a[i], b[i]), (reconst_mode, lost, need, i)
+
+
+@pytest.mark.parametrize("d,p", [(10, 4), (6, 3), (4, 2), (14, 2), (3, 9)])
+def test_reconst_other_configs_both_paths(rng, reconst_mode, d, p):
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    for _ in range(20):
+        v = [rng.integers(0, 256, size=1024, dtype=np.uint8) for _ in range(d)]
+        v += [np.zeros(1024, np.uint8) for _ in range(p)]
+        o.encode(v)
+        lost = [int(t) for t in rng.permutation(d + p)[: int(rng.integers(1, p + 1))]]
+        need = lost[: int(rng.integers(0, len(lost) + 1))]
+        has = [i for i in range(d + p) if i not in lost]
+        a = [r.copy() for r in v]
+        b = [r.copy() for r in v]
+        x.reconst(a, has, need)
+        o.reconst(b, has, need)
+        for i in range(d + p):
+            assert np.array_equal(a[i], b[i]), (reconst_mode, d, p, lost, need, i)

@@ -22,6 +22,11 @@
 //    runtime-count variants.  Misaligned / odd sizes take a byte-granular path.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "gf256.h"
 #include "xrs_plan.h"
 
 namespace xrs {
@@ -340,8 +345,133 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
   for (int r = 0; r < R; ++r) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
 }
 
+// ============================================================ mix kernel
+// General Reconst in one pass: out_r = sum_c ca[r][c]*a_c ^ cb[r][c]*b_c.
+// Sources are read once each (only the halves `use` asks for); zero
+// coefficients are skipped with wave-uniform branches, 1 is a plain XOR.
+struct MixArgs {
+  RowRef src[kMixSrc];
+  uint32_t use[kMixSrc];
+  RowRef dst[kMixOut];
+  uint8_t ca[kMixOut][kMixSrc];
+  uint8_t cb[kMixOut][kMixSrc];
+  const GfTab* tabs;  // device table, tabs[c] = GfTab of coefficient c
+  int n_out, n_src;
+  uint64_t half, chunks, total;
+};
+
+template <int R, int W>
+__device__ __forceinline__ void mix_term(uint32_t (&acc)[R][W], int r, uint32_t k,
+                                         const GfTab* tabs, const uint32_t* x, const Sel* s) {
+  if (k == 0) return;
+  if (k == 1) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] ^= x[w];
+    return;
+  }
+  const GfTab t = tabs[k];
+#pragma unroll
+  for (int w = 0; w < W; ++w) acc[r][w] ^= gmul(t, s[w]);
+}
+
+template <int R, bool VEC>
+__global__ __launch_bounds__(kBlock) void mix_kernel(const MixArgs a) {
+  constexpr int W = VEC ? 4 : 1;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
+  uint32_t acc[R][W];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+  for (int c = 0; c < a.n_src; ++c) {
+    const uint64_t s = row_addr(a.src[c], stripe, off);
+    const uint32_t use = a.use[c];
+    uint32_t xa[W], xb[W];
+    Sel sa[W], sb[W];
+    if (use & 1u) {
+      ld<VEC>(xa, s, nb);
+#pragma unroll
+      for (int w = 0; w < W; ++w) sa[w] = sel_of(xa[w]);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < a.n_out) mix_term<R, W>(acc, r, a.ca[r][c], a.tabs, xa, sa);
+    }
+    if (use & 2u) {
+      ld<VEC>(xb, s + a.half, nb);
+#pragma unroll
+      for (int w = 0; w < W; ++w) sb[w] = sel_of(xb[w]);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < a.n_out) mix_term<R, W>(acc, r, a.cb[r][c], a.tabs, xb, sb);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (r < a.n_out) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
+}
+
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+// Per-device table of all 256 coefficients for the mix kernel (built once).
+const GfTab* device_tabs() {
+  static std::mutex mu;
+  static std::map<int, GfTab*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  GfTab host[256];
+  for (int c = 0; c < 256; ++c) host[c] = GF::get().tab(static_cast<uint8_t>(c));
+  GfTab* d = nullptr;
+  if (hipMalloc(&d, sizeof(host)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  cache[dev] = d;
+  return d;
+}
+
+template <int R, bool VEC>
+int launch_mix_t(const MixPlan& p, const GfTab* tabs, hipStream_t stream) {
+  MixArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int c = 0; c < p.n_src; ++c) {
+    a.src[c] = p.src[c];
+    a.use[c] = p.use[c];
+  }
+  for (int r = 0; r < p.n_out; ++r) {
+    a.dst[r] = p.dst[r];
+    for (int c = 0; c < p.n_src; ++c) {
+      a.ca[r][c] = p.ca[r][c];
+      a.cb[r][c] = p.cb[r][c];
+    }
+  }
+  a.tabs = tabs;
+  a.n_out = p.n_out;
+  a.n_src = p.n_src;
+  a.half = p.half;
+  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.total = a.chunks * p.n_stripes;
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((mix_kernel<R, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
+                     stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <bool VEC>
+int launch_mix_r(const MixPlan& p, const GfTab* tabs, hipStream_t s) {
+  if (p.n_out <= 4) return launch_mix_t<4, VEC>(p, tabs, s);
+  if (p.n_out <= 8) return launch_mix_t<8, VEC>(p, tabs, s);
+  return launch_mix_t<12, VEC>(p, tabs, s);
+}
 
 template <int P, int C, bool ACC, bool VEC>
 int launch_pair_t(const PairPlan& p, hipStream_t stream) {
@@ -440,6 +570,18 @@ int launch_pair(const PairPlan& p, void* stream) {
   for (int r = 0; r < p.P && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
   if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
   return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
+}
+
+int launch_mix(const MixPlan& p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.n_out < 1 || p.n_out > kMixOut || p.n_src < 1 || p.n_src > kMixSrc)
+    return static_cast<int>(hipErrorInvalidValue);
+  const GfTab* tabs = device_tabs();
+  if (!tabs) return static_cast<int>(hipErrorOutOfMemory);
+  bool vec = aligned16(p.half);
+  for (int c = 0; c < p.n_src && vec; ++c) vec = aligned16(p.src[c].ptr) && aligned16(p.src[c].stripe_stride);
+  for (int r = 0; r < p.n_out && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
+  return vec ? launch_mix_r<true>(p, tabs, s) : launch_mix_r<false>(p, tabs, s);
 }
 
 int launch_rows(const RowsPlan& p, void* stream) {

@@ -67,8 +67,28 @@ struct RowsPlan {
   uint64_t n_stripes;
 };
 
+// "mix" kernel: one pass for the whole general Reconst (xrs.go:236-301).
+// Sources are shards (a-half at ptr, b-half at ptr + half); every output is a
+// half-row written as sum_c ca[r][c]*a_c ^ cb[r][c]*b_c (dense, zero-skipped,
+// coefficient 1 is a plain XOR).  Coefficients index a device table of all
+// 256 GfTabs, so the plan itself stays small.
+constexpr int kMixOut = 12;
+constexpr int kMixSrc = 16;
+
+struct MixPlan {
+  int n_out, n_src;
+  RowRef src[kMixSrc];  // shard rows (a-half address)
+  uint8_t use[kMixSrc];  // bit 0: a-half read, bit 1: b-half read
+  RowRef dst[kMixOut];  // output half-rows
+  uint8_t ca[kMixOut][kMixSrc];
+  uint8_t cb[kMixOut][kMixSrc];
+  uint64_t half;
+  uint64_t n_stripes;
+};
+
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.
 int launch_pair(const PairPlan& plan, void* stream);
 int launch_rows(const RowsPlan& plan, void* stream);
+int launch_mix(const MixPlan& plan, void* stream);
 
 }  // namespace xrs

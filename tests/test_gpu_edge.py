@@ -83,10 +83,10 @@ def test_cpp_port_under_host_asan():
 
 @pytest.fixture(params=["fused", "stepwise"])
 def reconst_mode(request, monkeypatch):
-    if request.param == "stepwise":
-        monkeypatch.setenv("XRS_RECONST_STEPWISE", "1")
+    if request.param == "fused":
+        monkeypatch.setenv("XRS_RECONST_FUSED", "1")
     else:
-        monkeypatch.delenv("XRS_RECONST_STEPWISE", raising=False)
+        monkeypatch.delenv("XRS_RECONST_FUSED", raising=False)
     return request.param
 
 

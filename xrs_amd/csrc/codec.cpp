@@ -379,10 +379,13 @@ int reconst_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stri
                  Written* w) {
   const int d = x->d, p = x->p;
   const size_t half = size / 2;
-  // One fused pass when every step validates and the plan fits.
-  // XRS_RECONST_STEPWISE=1 forces the step-by-step path (tests cover both).
-  const char* sw = std::getenv("XRS_RECONST_STEPWISE");
-  if (!(sw && sw[0] == '1')) {
+  // XRS_RECONST_FUSED=1: one composed mix-kernel pass (when every step
+  // validates and the plan fits).  Measured slower than the step-by-step
+  // plan on 12+4 (expanding each lost a-half into every output that uses it
+  // triples the GF work; profiles/r01_bench_multi.log), so it is opt-in;
+  // tests run both paths.
+  const char* fz = std::getenv("XRS_RECONST_FUSED");
+  if (fz && fz[0] == '1') {
     std::vector<int> a_lost;
     for (int i = 0; i < d + p; ++i)
       if (std::find(dp_has, dp_has + n_has, i) == dp_has + n_has) a_lost.push_back(i);

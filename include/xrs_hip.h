@@ -139,6 +139,22 @@ void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin existing host memory */
 int xrs_host_unregister(void *p);
 
+/* ---- batching queue (per-stripe calls from many threads) --------------- *
+ * Coalesces concurrent per-stripe calls (Go: many goroutines calling
+ * x.Encode / x.ReconstOne) into device batches of up to max_batch_stripes
+ * (capped at 64 MiB of staging) with one H2D, one kernel and one D2H per
+ * batch.  A batch runs when full, or max_wait_us after it opened once every
+ * reserved stripe is staged.  Each call blocks until its own stripe is done
+ * and has the semantics of xrs_encode / xrs_reconst_one for vects of the
+ * queue's `size`.  Thread-safe; one queue per (codec, vect size). */
+typedef struct xrs_queue xrs_queue;
+int xrs_queue_new(const xrs_codec *codec, size_t size, size_t max_batch_stripes, int max_wait_us,
+                  xrs_queue **out);
+void xrs_queue_free(xrs_queue *q);
+int xrs_queue_encode(xrs_queue *q, uint8_t *const *vects, int n);
+int xrs_queue_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k);
+size_t xrs_queue_batch_stripes(const xrs_queue *q);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,61 @@
+"""GPU tests of the batching queue (xrs_queue_*): concurrent per-stripe calls
+from many threads, coalesced into device batches, bit-exact to the oracle."""
+import threading
+
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+pytestmark = pytest.mark.gpu
+D, P = 12, 4
+
+
+@pytest.mark.parametrize("size", [4096, 1030, 1 << 20])
+def test_queue_concurrent_encode_and_reconst(size):
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=64, max_wait_us=100)
+    n_threads, per_thread = (16, 24) if size < (1 << 20) else (8, 4)
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(1000 + t))
+        try:
+            for i in range(per_thread):
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D)]
+                v += [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(P)]
+                ref = [a.copy() for a in v]
+                o.encode(ref)
+                q.encode(v)
+                assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, i)
+                k = int(rng.integers(0, D))
+                a_need, b_need = x.get_need_vects(k)
+                v[k][:] = 0
+                for j in range(D + P):  # garbage outside the need set
+                    if j not in a_need and j != k:
+                        v[j][: size // 2] = 0xC3
+                q.reconst_one(v, k)
+                assert np.array_equal(v[k], ref[k]), ("rec", t, i, k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    q.close()
+    assert not errors, errors[:3]
+
+
+def test_queue_errors():
+    x = xrs_amd.XRS(D, P)
+    q = xrs_amd.XRSQueue(x, 64)
+    with pytest.raises(xrs_amd.XRSError, match="illegal data index: 12"):
+        q.reconst_one([np.zeros(64, np.uint8) for _ in range(16)], 12)
+    with pytest.raises(xrs_amd.XRSError, match="illegal vects"):
+        q.encode([np.zeros(64, np.uint8) for _ in range(15)])
+    with pytest.raises(xrs_amd.XRSError):
+        xrs_amd.XRSQueue(x, 63)
+    q.close()

@@ -1,0 +1,75 @@
+// sync_bench.cpp -- per-stripe drop-in call cost (xrs_encode / xrs_reconst_one
+// on host vects, like Go's x.Encode(vects)) and the batching queue
+// (xrs_queue_*) with T concurrent caller threads.
+//
+//   g++ -O2 -std=c++17 -Iinclude tools/sync_bench.cpp -Lxrs_amd -lxrs_hip \
+//       -Wl,-rpath,$PWD/xrs_amd -lpthread -o tools/sync_bench
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "xrs_hip.h"
+
+static double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
+  const int seconds = 2;
+  xrs_codec* c = nullptr;
+  if (xrs_new(12, 4, &c)) return 2;
+  // --- plain sync calls, one thread
+  {
+    std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, 1));
+    std::vector<uint8_t*> p;
+    for (auto& x : v) p.push_back(x.data());
+    xrs_encode(c, p.data(), 16, size);
+    long n = 0;
+    const double t0 = now();
+    while (now() - t0 < seconds) {
+      if (xrs_encode(c, p.data(), 16, size)) return 3;
+      ++n;
+    }
+    const double dt = (now() - t0) / n;
+    std::printf("{\"api\": \"xrs_encode\", \"vect_bytes\": %zu, \"threads\": 1, \"us_per_call\": %.1f, "
+                "\"gibps\": %.3f}\n", size, dt * 1e6, 16.0 * size / dt / (1 << 30));
+  }
+  // --- batching queue, T threads
+  for (int threads : {1, 8, 32, 128}) {
+    xrs_queue* q = nullptr;
+    if (xrs_queue_new(c, size, 1024, 50, &q)) return 4;
+    std::atomic<long> total{0};
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&, t] {
+        std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, (uint8_t)t));
+        std::vector<uint8_t*> p;
+        for (auto& x : v) p.push_back(x.data());
+        long n = 0;
+        while (!stop.load(std::memory_order_relaxed)) {
+          if (xrs_queue_encode(q, p.data(), 16)) std::abort();
+          ++n;
+        }
+        total += n;
+      });
+    const double t0 = now();
+    std::this_thread::sleep_for(std::chrono::seconds(seconds));
+    stop = true;
+    for (auto& x : th) x.join();
+    const double dt = now() - t0;
+    std::printf("{\"api\": \"xrs_queue_encode\", \"vect_bytes\": %zu, \"threads\": %d, "
+                "\"stripes_per_s\": %.0f, \"gibps\": %.3f}\n", size, threads, total / dt,
+                total * 16.0 * size / dt / (1 << 30));
+    std::fflush(stdout);
+    xrs_queue_free(q);
+  }
+  xrs_free(c);
+  std::fflush(stdout);
+  std::_Exit(0);
+}

@@ -16,7 +16,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-__all__ = ["XRS", "XRSError", "lib", "LIB_PATH", "batch_strides"]
+__all__ = ["XRS", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
@@ -70,6 +70,11 @@ def _load():
         "xrs_host_free": ([P], None),
         "xrs_host_register": ([P, Z], I),
         "xrs_host_unregister": ([P], I),
+        "xrs_queue_new": ([P, Z, Z, I, ctypes.POINTER(P)], I),
+        "xrs_queue_free": ([P], None),
+        "xrs_queue_encode": ([P, PP, I], I),
+        "xrs_queue_reconst_one": ([P, PP, I, I], I),
+        "xrs_queue_batch_stripes": ([P], Z),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -254,3 +259,34 @@ class XRS:
                                       parity_shard_stride, parity_stripe_stride, n_stripes, stream)
         bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
+
+
+class XRSQueue:
+    """Batching queue over a codec (xrs_queue_*): per-stripe Encode /
+    ReconstOne calls from many threads are coalesced into device batches.
+    ctypes releases the GIL during each call, so Python threads batch too."""
+
+    def __init__(self, codec: XRS, size: int, max_batch_stripes: int = 1024,
+                 max_wait_us: int = 50):
+        h = ctypes.c_void_p()
+        _raise(_lib.xrs_queue_new(codec.handle, size, max_batch_stripes, max_wait_us,
+                                  ctypes.byref(h)), size)
+        self._codec = codec  # keep the codec alive
+        self._h = h
+        self.size = size
+        self.batch_stripes = _lib.xrs_queue_batch_stripes(h)
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            _lib.xrs_queue_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def encode(self, vects) -> None:
+        _raise(_lib.xrs_queue_encode(self._h, _ptrs(vects), len(vects)), self.size)
+
+    def reconst_one(self, vects, need_reconst: int) -> None:
+        _raise(_lib.xrs_queue_reconst_one(self._h, _ptrs(vects), len(vects), int(need_reconst)),
+               need_reconst)

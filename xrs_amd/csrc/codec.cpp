@@ -676,6 +676,26 @@ bool vects_ok(uint8_t* const* v, int n) {
 
 }  // namespace
 
+// Entry points for the other translation units of the library (queue.cpp).
+namespace xrs_detail {
+int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+               size_t stripe_stride, size_t n_stripes, void* stream) {
+  return encode_impl(x, {base, shard_stride, stripe_stride}, size, n_stripes,
+                     static_cast<hipStream_t>(stream));
+}
+int reconst_one_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                    size_t stripe_stride, size_t n_stripes, int k, void* stream) {
+  return reconst_one_impl(x, {base, shard_stride, stripe_stride}, size, n_stripes, k,
+                          static_cast<hipStream_t>(stream));
+}
+int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi) {
+  return need_vects(x, k, a_need, bi);
+}
+int codec_device(const xrs_codec* x) { return x->device; }
+int codec_d(const xrs_codec* x) { return x->d; }
+int codec_p(const xrs_codec* x) { return x->p; }
+}  // namespace xrs_detail
+
 // ====================================================================== C ABI
 extern "C" {
 

@@ -1,0 +1,308 @@
+// queue.cpp -- batching queue behind the per-stripe drop-in calls.
+//
+// A Go storage server calls x.Encode(vects) / x.ReconstOne(vects, k) per
+// stripe from many goroutines.  One GPU launch per 4 KiB
+// stripe is latency bound, so the queue coalesces concurrent per-stripe calls
+// into device batches:
+//
+//   caller thread: reserve a slot in the open batch -> copy its vects into the
+//     batch's pinned staging (callers copy in parallel) -> wait -> copy its
+//     outputs back -> release the slot.
+//   worker threads (2): run a batch when it is full, or when it has waited
+//     max_wait_us with every reserved slot filled: one H2D of the whole batch,
+//     one kernel over all its stripes, one D2H, on the batch's own stream.
+//
+// Every stripe's arithmetic is the batched device path (encode_dev /
+// reconst_one_dev); results are bit-identical to the per-stripe calls.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "xrs_hip.h"
+
+namespace xrs_detail {
+int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+               size_t stripe_stride, size_t n_stripes, void* stream);
+int reconst_one_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                    size_t stripe_stride, size_t n_stripes, int k, void* stream);
+int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi);
+int codec_device(const xrs_codec* x);
+int codec_d(const xrs_codec* x);
+int codec_p(const xrs_codec* x);
+}  // namespace xrs_detail
+
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+constexpr int kBatches = 4;
+constexpr int kWorkers = 2;
+constexpr size_t kMaxBatchBytes = 64u << 20;
+
+enum State { FREE, OPEN, CLOSED, RUNNING, DONE };
+
+struct Batch {
+  uint8_t* host = nullptr;  // pinned staging, compact [stripe][shard][size]
+  uint8_t* dev = nullptr;
+  hipStream_t stream = nullptr;
+  State state = FREE;
+  int key = -1;  // 0: encode, 1 + k: reconst_one(k)
+  size_t reserved = 0, filled = 0, released = 0;
+  uint64_t gen = 0;
+  int err = 0;
+  Clock::time_point opened;
+};
+
+}  // namespace
+
+struct xrs_queue {
+  const xrs_codec* codec = nullptr;
+  int d = 0, p = 0, device = -1;
+  size_t size = 0, stripe_bytes = 0, max_batch = 1;
+  std::chrono::microseconds max_wait{50};
+  Batch b[kBatches];
+  int open = -1;
+  bool stop = false;
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done, cv_free;
+  std::thread worker[kWorkers];
+
+  void run(int i);
+  void work();
+  int submit(int key, uint8_t* const* vects, int n);
+};
+
+void xrs_queue::run(int i) {
+  Batch& bt = b[i];
+  const size_t n = bt.reserved;
+  // Encode: only the data rows go up and only the parity rows come back (one
+  // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back.
+  const size_t up_off = 0, up_len = bt.key == 0 ? static_cast<size_t>(d) * size : stripe_bytes;
+  const size_t dn_off = bt.key == 0 ? static_cast<size_t>(d) * size
+                                    : static_cast<size_t>(bt.key - 1) * size;
+  const size_t dn_len = bt.key == 0 ? static_cast<size_t>(p) * size : size;
+  int e = 0;
+  if (hipMemcpy2DAsync(bt.dev + up_off, stripe_bytes, bt.host + up_off, stripe_bytes, up_len, n,
+                       hipMemcpyHostToDevice, bt.stream) != hipSuccess)
+    e = XRS_ERR_HIP;
+  if (!e) {
+    e = bt.key == 0 ? xrs_detail::encode_dev(codec, bt.dev, size, size, stripe_bytes, n, bt.stream)
+                    : xrs_detail::reconst_one_dev(codec, bt.dev, size, size, stripe_bytes, n,
+                                                  bt.key - 1, bt.stream);
+  }
+  if (!e && hipMemcpy2DAsync(bt.host + dn_off, stripe_bytes, bt.dev + dn_off, stripe_bytes, dn_len,
+                             n, hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
+    e = XRS_ERR_HIP;
+  if (hipStreamSynchronize(bt.stream) != hipSuccess && !e) e = XRS_ERR_HIP;
+  std::lock_guard<std::mutex> lk(mu);
+  bt.err = e;
+  bt.state = DONE;
+  cv_done.notify_all();
+}
+
+void xrs_queue::work() {
+  if (device >= 0) (void)hipSetDevice(device);
+  std::unique_lock<std::mutex> lk(mu);
+  while (!stop) {
+    int pick = -1;
+    Clock::time_point next = Clock::now() + max_wait;
+    for (int i = 0; i < kBatches && pick < 0; ++i) {
+      Batch& bt = b[i];
+      if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
+      if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
+        const auto due = bt.opened + max_wait;
+        if (Clock::now() >= due) {
+          bt.state = CLOSED;
+          if (open == i) open = -1;
+          pick = i;
+        } else {
+          next = std::min(next, due);
+        }
+      }
+    }
+    if (pick < 0) {
+      cv_work.wait_until(lk, next);
+      continue;
+    }
+    b[pick].state = RUNNING;
+    lk.unlock();
+    run(pick);
+    lk.lock();
+  }
+}
+
+int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
+  if (!vects || n != d + p) return XRS_ERR_ILLEGAL_VECTS;
+  for (int i = 0; i < n; ++i)
+    if (!vects[i]) return XRS_ERR_INVALID_ARG;
+  std::vector<std::pair<int, int>> in, out;  // (shard, 0 a / 1 b / 2 whole)
+  if (key == 0) {
+    for (int j = 0; j < d; ++j) in.push_back({j, 2});
+    for (int r = 0; r < p; ++r) out.push_back({d + r, 2});
+  } else {
+    const int k = key - 1;
+    std::vector<int> a_need;
+    int bi = 0;
+    const int e = xrs_detail::need_set(codec, k, &a_need, &bi);
+    if (e) return e;
+    for (int m = 0; m < d; ++m) in.push_back({m == k ? d : m, 1});
+    in.push_back({bi, 1});
+    for (int a : a_need) in.push_back({a, 0});
+    out.push_back({k, 2});
+  }
+  const size_t half = size / 2;
+  auto piece = [&](const std::pair<int, int>& pc, size_t* off, size_t* len) {
+    *off = pc.second == 1 ? half : 0;
+    *len = pc.second == 2 ? size : half;
+  };
+  int bi;
+  size_t slot;
+  uint64_t gen;
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      if (stop) return XRS_ERR_INVALID_ARG;
+      if (open >= 0 && b[open].key == key && b[open].reserved < max_batch) break;
+      if (open >= 0) {  // different op or full: close it, the worker runs it
+        b[open].state = CLOSED;
+        open = -1;
+        cv_work.notify_all();
+      }
+      int f = -1;
+      for (int i = 0; i < kBatches && f < 0; ++i)
+        if (b[i].state == FREE) f = i;
+      if (f < 0) {
+        cv_free.wait(lk);
+        continue;
+      }
+      Batch& nb = b[f];
+      nb.state = OPEN;
+      nb.key = key;
+      nb.reserved = nb.filled = nb.released = 0;
+      nb.err = 0;
+      nb.opened = Clock::now();
+      open = f;
+    }
+    bi = open;
+    slot = b[bi].reserved++;
+    gen = b[bi].gen;
+    if (b[bi].reserved == max_batch) {
+      b[bi].state = CLOSED;
+      open = -1;
+    }
+  }
+  Batch& bt = b[bi];
+  uint8_t* st = bt.host + slot * stripe_bytes;
+  for (auto& pc : in) {
+    size_t off, len;
+    piece(pc, &off, &len);
+    std::memcpy(st + static_cast<size_t>(pc.first) * size + off, vects[pc.first] + off, len);
+  }
+  int err;
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    bt.filled++;
+    cv_work.notify_all();
+    cv_done.wait(lk, [&] { return bt.gen == gen && bt.state == DONE; });
+    err = bt.err;
+  }
+  if (!err)
+    for (auto& pc : out) {
+      size_t off, len;
+      piece(pc, &off, &len);
+      std::memcpy(vects[pc.first] + off, st + static_cast<size_t>(pc.first) * size + off, len);
+    }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (++bt.released == bt.reserved) {
+      bt.state = FREE;
+      bt.gen++;
+      cv_free.notify_all();
+    }
+  }
+  return err;
+}
+
+extern "C" {
+
+int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes, int max_wait_us,
+                  xrs_queue** out) {
+  if (!codec || !out || (size & 1) || size == 0 || max_wait_us < 0) return XRS_ERR_INVALID_ARG;
+  *out = nullptr;
+  const int dev = xrs_detail::codec_device(codec);
+  if (dev < 0) return XRS_ERR_NO_DEVICE;
+  auto* q = new xrs_queue();
+  q->codec = codec;
+  q->d = xrs_detail::codec_d(codec);
+  q->p = xrs_detail::codec_p(codec);
+  q->device = dev;
+  q->size = size;
+  q->stripe_bytes = static_cast<size_t>(q->d + q->p) * size;
+  q->max_batch = std::max<size_t>(
+      1, std::min(max_batch_stripes ? max_batch_stripes : SIZE_MAX, kMaxBatchBytes / q->stripe_bytes));
+  q->max_wait = std::chrono::microseconds(max_wait_us);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(dev);
+  int e = XRS_OK;
+  for (Batch& bt : q->b) {
+    if (hipHostMalloc(&bt.host, q->max_batch * q->stripe_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&bt.dev, q->max_batch * q->stripe_bytes) != hipSuccess ||
+        hipStreamCreateWithFlags(&bt.stream, hipStreamNonBlocking) != hipSuccess) {
+      e = XRS_ERR_HIP;
+      break;
+    }
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (e) {
+    xrs_queue_free(q);
+    return e;
+  }
+  for (auto& w : q->worker) w = std::thread([q] { q->work(); });
+  *out = q;
+  return XRS_OK;
+}
+
+void xrs_queue_free(xrs_queue* q) {
+  if (!q) return;
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->stop = true;
+    q->cv_work.notify_all();
+  }
+  for (auto& w : q->worker)
+    if (w.joinable()) w.join();
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (q->device >= 0) (void)hipSetDevice(q->device);
+  for (Batch& bt : q->b) {
+    if (bt.stream) (void)hipStreamDestroy(bt.stream);
+    if (bt.dev) (void)hipFree(bt.dev);
+    if (bt.host) (void)hipHostFree(bt.host);
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  delete q;
+}
+
+// xrs.go:103 Encode, coalesced with concurrent callers.
+int xrs_queue_encode(xrs_queue* q, uint8_t* const* vects, int n) {
+  if (!q) return XRS_ERR_INVALID_ARG;
+  return q->submit(0, vects, n);
+}
+
+// xrs.go:175 ReconstOne, coalesced (only the GetNeedVects set is copied).
+int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
+  if (!q) return XRS_ERR_INVALID_ARG;
+  if (k < 0 || k >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  return q->submit(1 + k, vects, n);
+}
+
+size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }
+
+}  // extern "C"

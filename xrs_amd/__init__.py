@@ -268,6 +268,7 @@ class XRSQueue:
 
     def __init__(self, codec: XRS, size: int, max_batch_stripes: int = 1024,
                  max_wait_us: int = 50):
+        self._h = None
         h = ctypes.c_void_p()
         _raise(_lib.xrs_queue_new(codec.handle, size, max_batch_stripes, max_wait_us,
                                   ctypes.byref(h)), size)

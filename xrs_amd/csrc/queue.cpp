@@ -57,6 +57,7 @@ struct Batch {
   uint64_t gen = 0;
   int err = 0;
   Clock::time_point opened;
+  std::condition_variable done;  // this batch's waiters only (no thundering herd)
 };
 
 }  // namespace
@@ -70,7 +71,7 @@ struct xrs_queue {
   int open = -1;
   bool stop = false;
   std::mutex mu;
-  std::condition_variable cv_work, cv_done, cv_free;
+  std::condition_variable cv_work, cv_free;
   std::thread worker[kWorkers];
 
   void run(int i);
@@ -103,7 +104,7 @@ void xrs_queue::run(int i) {
   std::lock_guard<std::mutex> lk(mu);
   bt.err = e;
   bt.state = DONE;
-  cv_done.notify_all();
+  bt.done.notify_all();
 }
 
 void xrs_queue::work() {
@@ -207,9 +208,10 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
   int err;
   {
     std::unique_lock<std::mutex> lk(mu);
-    bt.filled++;
-    cv_work.notify_all();
-    cv_done.wait(lk, [&] { return bt.gen == gen && bt.state == DONE; });
+    // Wake a worker only when this fill makes the batch runnable (closed, or
+    // open with every reservation staged: the worker's timer then applies).
+    if (++bt.filled == bt.reserved) cv_work.notify_one();
+    bt.done.wait(lk, [&] { return bt.gen == gen && bt.state == DONE; });
     err = bt.err;
   }
   if (!err)

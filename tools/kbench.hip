@@ -211,6 +211,92 @@ __global__ __launch_bounds__(256) void enc_wouter(const PairArgs<4, 12, true> a)
   }
 }
 
+// Read-ceiling probes: U independent 16-B nt loads per lane (one-shot grid),
+// and an LDS-DMA (global_load_lds_dwordx4) stream into a per-wave LDS ring.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_u(const u32x4* __restrict__ a, uint64_t n, uint32_t* sink) {
+  const uint64_t base = (static_cast<uint64_t>(blockIdx.x) * 256 * U) + threadIdx.x;
+  u32x4 s = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t i = base + u * 256;
+    if (i < n) {
+      const gu32x4* p = (const gu32x4*)(a + i);
+      s ^= NT ? __builtin_nontemporal_load(p) : *p;
+    }
+  }
+  if ((s.x ^ s.y ^ s.z ^ s.w) == 0x12345678u) sink[0] = 1;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void read_glds(const u32x4* __restrict__ a, uint64_t n, uint32_t* sink) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * U * 1024];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const uint64_t base = (static_cast<uint64_t>(blockIdx.x) * 256 * U) + wave * 64 + lane;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t i = base + u * 256;
+    if (i < n)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a + i),
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * U + u) * 1024),
+                                       16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (lds[threadIdx.x * 16] == 0x5a && lds[threadIdx.x * 16 + 1] == 0x5a && sink[0] == 7) sink[1] = 1;
+}
+
+// ReconstOne / Encode address patterns split into their read and write parts.
+template <bool READ, bool WRITE>
+__global__ __launch_bounds__(256) void r1_rw(const RowsArgs<2, 12, 4, true> a, uint32_t* sink) {
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  u32x4 s0 = {0, 0, 0, 0}, s1 = {1, 2, 3, 4};
+  if (READ) {
+#pragma unroll
+    for (int m = 0; m < 12; ++m)
+      s0 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.msrc[m], stripe, off)));
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      s1 ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(row_addr(a.xsrc[x], stripe, off)));
+  }
+  if (WRITE) {
+    __builtin_nontemporal_store(s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[0], stripe, off)));
+    __builtin_nontemporal_store(s1 ^ s0, reinterpret_cast<gu32x4*>(row_addr(a.dst[1], stripe, off)));
+  } else if ((s0.x ^ s1.y) == 0x12345678u) {
+    sink[0] = 1;
+  }
+}
+
+template <bool READ, bool WRITE>
+__global__ __launch_bounds__(256) void enc_rw(const PairArgs<4, 12, true> a, uint32_t* sink) {
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  u32x4 sa = {0, 0, 0, 0}, sb = {1, 2, 3, 4};
+  if (READ) {
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      const uint64_t s = row_addr(a.src[c], stripe, off);
+      sa ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s));
+      sb ^= __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(s + a.half));
+    }
+  }
+  if (WRITE) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t d = row_addr(a.dst[r], stripe, off);
+      __builtin_nontemporal_store(sa + r, reinterpret_cast<gu32x4*>(d));
+      __builtin_nontemporal_store(sb + r, reinterpret_cast<gu32x4*>(d + a.half));
+    }
+  } else if ((sa.x ^ sb.y) == 0x12345678u) {
+    sink[0] = 1;
+  }
+}
+
 // Grid-stride XOR-only probes (memory ceiling with a persistent-style grid).
 __global__ __launch_bounds__(256) void r1_xor_gs(const RowsArgs<2, 12, 4, true> a) {
   for (uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; gid < a.total;
@@ -627,6 +713,97 @@ int main(int argc, char** argv) {
   if (which == "padab") {
     for (uint64_t S : {4096ull, 65536ull, 1ull << 20, 8ull << 20})
       pad_ab(tm, S, {0, 128, 256, 512, 4096 + 256}, 7);
+    return 0;
+  }
+  if (which == "rw") {
+    // same setup as "gs": ReconstOne 1 MiB pad 256, Encode 4 KiB pad 0
+    const uint64_t S1 = 1 << 20, n1 = 256, H1 = S1 / 2, sh1 = S1 + 256, st1 = 16 * sh1;
+    const uint64_t S2 = 4096, n2 = 65536, H2 = S2 / 2, st2 = 16 * S2;
+    uint8_t *b1, *b2;
+    uint32_t* sink;
+    CK(hipMalloc(&b1, n1 * st1));
+    CK(hipMalloc(&b2, n2 * st2));
+    CK(hipMalloc(&sink, 64));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)b1, n1 * st1 / 4, 5u);
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)b2, n2 * st2 / 4, 6u);
+    const uint64_t base1 = reinterpret_cast<uint64_t>(b1), base2 = reinterpret_cast<uint64_t>(b2);
+    RowsArgs<2, 12, 4, true> ra;
+    std::memset(&ra, 0, sizeof(ra));
+    for (int m = 0; m < 12; ++m) {
+      ra.msrc[m] = {base1 + (m == 0 ? 12 : m) * sh1 + H1, st1};
+      for (int r = 0; r < 2; ++r) ra.tab[m][r] = gf.tab(static_cast<uint8_t>(17 * m + 5 * r + 3));
+    }
+    ra.xsrc[0] = {base1 + 13 * sh1 + H1, st1};
+    for (int x = 1; x < 4; ++x) ra.xsrc[x] = {base1 + 3 * x * sh1, st1};
+    for (int x = 0; x < 4; ++x) ra.xmask[x] = 2;
+    ra.dst[0] = {base1 + H1, st1};
+    ra.dst[1] = {base1, st1};
+    ra.nm = 12; ra.nx = 4; ra.len = H1; ra.chunks = H1 / 16; ra.total = ra.chunks * n1;
+    PairArgs<4, 12, true> pa;
+    std::memset(&pa, 0, sizeof(pa));
+    for (int c = 0; c < 12; ++c) {
+      pa.src[c] = {base2 + c * S2, st2};
+      for (int r = 0; r < 4; ++r) pa.tab[c][r] = gf.tab(gf.inv(static_cast<uint8_t>((12 + r) ^ c)));
+    }
+    for (int r = 0; r < 4; ++r) pa.dst[r] = {base2 + (12 + r) * S2, st2};
+    pa.n_src = 12; pa.half = H2; pa.chunks = H2 / 16; pa.total = pa.chunks * n2;
+    const unsigned bl1 = (unsigned)(ra.total / 256), bl2 = (unsigned)(pa.total / 256);
+    std::vector<double> t[8];
+    for (int round = 0; round < 5; ++round) {
+      t[0].push_back(tm.ms([&] { hipLaunchKernelGGL((rows_kernel<2, 12, 4, false, true>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+      t[1].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_rw<true, true>), dim3(bl1), dim3(256), 0, 0, ra, sink); }, 5));
+      t[2].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_rw<true, false>), dim3(bl1), dim3(256), 0, 0, ra, sink); }, 5));
+      t[3].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_rw<false, true>), dim3(bl1), dim3(256), 0, 0, ra, sink); }, 5));
+      t[4].push_back(tm.ms([&] { hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+      t[5].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
+      t[6].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, false>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
+      t[7].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<false, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
+    }
+    const char* nm[8] = {"r1 product", "r1 read+write (xor)", "r1 read only (16 rows)", "r1 write only (2 rows)",
+                         "enc product", "enc read+write (xor)", "enc read only (24 halves)", "enc write only (8 halves)"};
+    const double by[8] = {9.0 * S1 * n1, 9.0 * S1 * n1, 8.0 * S1 * n1, 1.0 * S1 * n1,
+                          16.0 * S2 * n2, 16.0 * S2 * n2, 12.0 * S2 * n2, 4.0 * S2 * n2};
+    for (int i = 0; i < 8; ++i) {
+      std::sort(t[i].begin(), t[i].end());
+      report(nm[i], t[i][2], by[i]);
+    }
+    return 0;
+  }
+  if (which == "readceil") {
+    const uint64_t bytes = 8ull << 30, n = bytes / 16;
+    uint8_t* a;
+    uint32_t* sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(sink, 0, 64));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (uint32_t*)a, bytes / 4, 1u);
+    const u32x4* p = (const u32x4*)a;
+    std::vector<double> t[9];
+    const char* nm[9] = {"read U=1 plain", "read U=1 nt", "read U=4 nt", "read U=8 nt", "read U=4 plain",
+                         "glds U=1", "glds U=4", "glds U=8", "copy float4 g=65536"};
+    uint8_t* b;
+    CK(hipMalloc(&b, bytes));
+    for (int r = 0; r < 5; ++r) {
+      t[0].push_back(tm.ms([&] { hipLaunchKernelGGL((read_u<1, false>), dim3(n / 256), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[1].push_back(tm.ms([&] { hipLaunchKernelGGL((read_u<1, true>), dim3(n / 256), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[2].push_back(tm.ms([&] { hipLaunchKernelGGL((read_u<4, true>), dim3(n / 1024), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[3].push_back(tm.ms([&] { hipLaunchKernelGGL((read_u<8, true>), dim3(n / 2048), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[4].push_back(tm.ms([&] { hipLaunchKernelGGL((read_u<4, false>), dim3(n / 1024), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[5].push_back(tm.ms([&] { hipLaunchKernelGGL((read_glds<1>), dim3(n / 256), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[6].push_back(tm.ms([&] { hipLaunchKernelGGL((read_glds<4>), dim3(n / 1024), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[7].push_back(tm.ms([&] { hipLaunchKernelGGL((read_glds<8>), dim3(n / 2048), dim3(256), 0, 0, p, n, sink); }, 5));
+      t[8].push_back(tm.ms([&] { hipLaunchKernelGGL(copy_kernel, dim3(65536), dim3(256), 0, 0, p, (u32x4*)b, n); }, 5));
+    }
+    for (int i = 0; i < 9; ++i) {
+      std::sort(t[i].begin(), t[i].end());
+      report(nm[i], t[i][2], i == 8 ? 2.0 * bytes : 1.0 * bytes);
+    }
+    return 0;
+  }
+  if (which == "padfine") {  // 1 MiB vects, finer pad sweep
+    pad_ab(tm, 1ull << 20, {192, 256, 320, 384, 640, 768}, 7);
+    pad_ab(tm, 1ull << 20, {256, 1280, 1536, 2304, 3328, 6400}, 7);
+    pad_ab(tm, 4096, {0, 64, 128, 192, 320}, 7);
     return 0;
   }
   if (which == "sweep") {

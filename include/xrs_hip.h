@@ -123,6 +123,22 @@ int xrs_replace_batched(const xrs_codec *codec, const uint8_t *data_base,
                         int n, size_t size, uint8_t *parity_base, size_t parity_shard_stride,
                         size_t parity_stripe_stride, size_t n_stripes, void *stream);
 
+/* ---- per-shard pointer tables (device memory, async) -------------------- *
+ * shards[i] = base of shard i; stripe s of shard i at shards[i] + s*stripe_stride.
+ * For shards held in separate allocations (e.g. one buffer per disk), or on
+ * peer GPUs: with xrs_enable_peer_access(device, peer) the kernels read (and
+ * write) peer HBM directly over xGMI (cross-GPU repair). */
+int xrs_encode_shards(const xrs_codec *codec, uint8_t *const *shards, size_t stripe_stride,
+                      size_t size, size_t n_stripes, void *stream);
+/* Only shards in the GetNeedVects set and shard k are dereferenced (others may be NULL). */
+int xrs_reconst_one_shards(const xrs_codec *codec, uint8_t *const *shards, size_t stripe_stride,
+                           size_t size, size_t n_stripes, int k, void *stream);
+int xrs_reconst_shards(const xrs_codec *codec, uint8_t *const *shards, size_t stripe_stride,
+                       size_t size, size_t n_stripes, const int *dp_has, int n_has,
+                       const int *need, int n_need, void *stream);
+/* Let kernels running on `device` access HBM of `peer` (idempotent). */
+int xrs_enable_peer_access(int device, int peer);
+
 /* ---- host-resident batches (pipelined, synchronous) -------------------- *
  * The real caller's path (shards start and end in host memory, e.g. disk or
  * NIC buffers): stripes are moved in chunks through device slots on three

@@ -70,6 +70,10 @@ def _load():
         "xrs_host_free": ([P], None),
         "xrs_host_register": ([P, Z], I),
         "xrs_host_unregister": ([P], I),
+        "xrs_encode_shards": ([P, PP, Z, Z, Z, P], I),
+        "xrs_reconst_one_shards": ([P, PP, Z, Z, Z, I, P], I),
+        "xrs_reconst_shards": ([P, PP, Z, Z, Z, IP, I, IP, I, P], I),
+        "xrs_enable_peer_access": ([I, I], I),
         "xrs_queue_new": ([P, Z, Z, I, ctypes.POINTER(P)], I),
         "xrs_queue_free": ([P], None),
         "xrs_queue_encode": ([P, PP, I], I),
@@ -207,6 +211,28 @@ class XRS:
                               _ptrs(parity), len(parity))
         bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
+
+    # ------------------------------------------- per-shard pointer tables
+    # shards: list of d+p device addresses (int); stripe s of shard i at
+    # shards[i] + s*stripe_stride.  Shards may live on peer GPUs (xGMI).
+    def encode_shards(self, shards, stripe_stride: int, size: int, n_stripes: int,
+                      stream: int = 0) -> None:
+        t = (ctypes.c_void_p * len(shards))(*shards)
+        _raise(_lib.xrs_encode_shards(self._h, t, stripe_stride, size, n_stripes, stream), size)
+
+    def reconst_one_shards(self, shards, stripe_stride: int, size: int, n_stripes: int, k: int,
+                           stream: int = 0) -> None:
+        t = (ctypes.c_void_p * len(shards))(*[s or 0 for s in shards])
+        rc = _lib.xrs_reconst_one_shards(self._h, t, stripe_stride, size, n_stripes, int(k), stream)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else k)
+
+    def reconst_shards(self, shards, stripe_stride: int, size: int, n_stripes: int, dp_has,
+                       need_reconst, stream: int = 0) -> None:
+        t = (ctypes.c_void_p * len(shards))(*shards)
+        rc = _lib.xrs_reconst_shards(self._h, t, stripe_stride, size, n_stripes, _ints(dp_has),
+                                     len(dp_has), _ints(need_reconst), len(need_reconst), stream)
+        arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
 
     # ------------------------------------------- host-resident pipelined API
     # host_base: address of a host buffer (pinned for full PCIe rate).

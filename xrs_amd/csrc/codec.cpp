@@ -152,13 +152,19 @@ int run_rows(const std::vector<RowRef>& dst, const std::vector<MulSrc>& msrc,
   return XRS_OK;
 }
 
-// Device layout of a batch of stripes.
+// Device layout of a batch of stripes: shard i of stripe s at
+// base + s*stripe_stride + i*shard_stride, or, with a per-shard pointer table,
+// at table[i] + s*stripe_stride (shards in separate allocations, or on peer
+// GPUs reached over xGMI).
 struct Layout {
   uint8_t* base;
   size_t shard_stride, stripe_stride;
+  const uint64_t* table = nullptr;
   RowRef row(int shard, size_t off) const {
-    return {reinterpret_cast<uint64_t>(base) + static_cast<uint64_t>(shard) * shard_stride + off,
-            static_cast<uint64_t>(stripe_stride)};
+    const uint64_t b = table ? table[shard]
+                             : reinterpret_cast<uint64_t>(base) +
+                                   static_cast<uint64_t>(shard) * shard_stride;
+    return {b + off, static_cast<uint64_t>(stripe_stride)};
   }
 };
 
@@ -901,6 +907,85 @@ int xrs_replace_batched(const xrs_codec* x, const uint8_t* data_base, size_t dat
   return replace_impl(x, {const_cast<uint8_t*>(data_base), data_shard_stride, data_stripe_stride},
                       rows, n, size, {parity_base, parity_shard_stride, parity_stripe_stride},
                       n_stripes, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------ per-shard pointer tables
+static bool table_ok(uint8_t* const* shards, int n) {
+  if (!shards) return false;
+  for (int i = 0; i < n; ++i)
+    if (!shards[i]) return false;
+  return true;
+}
+
+int xrs_encode_shards(const xrs_codec* x, uint8_t* const* shards, size_t stripe_stride,
+                      size_t size, size_t n_stripes, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!table_ok(shards, x->d + x->p)) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  std::vector<uint64_t> t(shards, shards + x->d + x->p);
+  for (int i = 0; i < x->d + x->p; ++i) t[i] = reinterpret_cast<uint64_t>(shards[i]);
+  return encode_impl(x, {nullptr, 0, stripe_stride, t.data()}, size, n_stripes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int xrs_reconst_one_shards(const xrs_codec* x, uint8_t* const* shards, size_t stripe_stride,
+                           size_t size, size_t n_stripes, int k, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (k < 0 || k >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!shards) return XRS_ERR_INVALID_ARG;
+  std::vector<int> a_need;
+  int bi = 0;
+  need_vects(x, k, &a_need, &bi);
+  // Only the GetNeedVects set and vect k must be valid pointers.
+  std::vector<uint64_t> t(x->d + x->p, 0);
+  std::vector<int> used = {k, x->d, bi};
+  for (int m = 0; m < x->d; ++m) used.push_back(m);
+  for (int a : a_need) used.push_back(a);
+  for (int i : used) {
+    if (!shards[i]) return XRS_ERR_INVALID_ARG;
+    t[i] = reinterpret_cast<uint64_t>(shards[i]);
+  }
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  return reconst_one_impl(x, {nullptr, 0, stripe_stride, t.data()}, size, n_stripes, k,
+                          static_cast<hipStream_t>(stream));
+}
+
+int xrs_reconst_shards(const xrs_codec* x, uint8_t* const* shards, size_t stripe_stride,
+                       size_t size, size_t n_stripes, const int* dp_has, int n_has,
+                       const int* need, int n_need, void* stream) {
+  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] < x->d)
+    return xrs_reconst_one_shards(x, shards, stripe_stride, size, n_stripes, need[0], stream);
+  int e = check_size(size);
+  if (e) return e;
+  if (!table_ok(shards, x->d + x->p)) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  std::vector<uint64_t> t(x->d + x->p);
+  for (int i = 0; i < x->d + x->p; ++i) t[i] = reinterpret_cast<uint64_t>(shards[i]);
+  Written w;
+  return reconst_impl(x, {nullptr, 0, stripe_stride, t.data()}, size, size ? n_stripes : 0,
+                      dp_has, n_has, need, n_need, static_cast<hipStream_t>(stream), &w);
+}
+
+int xrs_enable_peer_access(int device, int peer) {
+  int prev = -1, can = 0;
+  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess || !can) return XRS_ERR_INVALID_ARG;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return XRS_ERR_HIP;
+  hipError_t r = hipDeviceEnablePeerAccess(peer, 0);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (r == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return XRS_OK;
+  }
+  return hip_err(r);
 }
 
 // ------------------------------------------------------ host-resident batches

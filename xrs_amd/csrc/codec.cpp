@@ -925,7 +925,7 @@ int xrs_encode_shards(const xrs_codec* x, uint8_t* const* shards, size_t stripe_
   if (n_stripes == 0 || size == 0) return XRS_OK;
   if (!table_ok(shards, x->d + x->p)) return XRS_ERR_INVALID_ARG;
   if (x->device < 0) return XRS_ERR_NO_DEVICE;
-  std::vector<uint64_t> t(shards, shards + x->d + x->p);
+  std::vector<uint64_t> t(x->d + x->p);
   for (int i = 0; i < x->d + x->p; ++i) t[i] = reinterpret_cast<uint64_t>(shards[i]);
   return encode_impl(x, {nullptr, 0, stripe_stride, t.data()}, size, n_stripes,
                      static_cast<hipStream_t>(stream));

@@ -297,79 +297,6 @@ __global__ __launch_bounds__(256) void enc_rw(const PairArgs<4, 12, true> a, uin
   }
 }
 
-// Cache-policy probes: the XOR-only ReconstOne pattern with the store (SP)
-// and load (LP) cache bits chosen by inline asm.  0: none, 1: nt, 2: sc1,
-// 3: sc0 sc1, 4: sc0 sc1 nt, 5: sc0.
-template <int POL>
-__device__ __forceinline__ void st_pol(uint64_t addr, u32x4 v) {
-  if constexpr (POL == 0) asm volatile("global_store_dwordx4 %0, %1, off" :: "v"(addr), "v"(v) : "memory");
-  if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(addr), "v"(v) : "memory");
-  if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(addr), "v"(v) : "memory");
-  if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(addr), "v"(v) : "memory");
-  if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(addr), "v"(v) : "memory");
-  if constexpr (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0" :: "v"(addr), "v"(v) : "memory");
-}
-template <int POL>
-__device__ __forceinline__ u32x4 ld_pol(uint64_t addr) {
-  u32x4 v;
-  if constexpr (POL == 0) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(addr) : "memory");
-  if constexpr (POL == 1) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(addr) : "memory");
-  if constexpr (POL == 2) asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(addr) : "memory");
-  if constexpr (POL == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(addr) : "memory");
-  if constexpr (POL == 4) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(v) : "v"(addr) : "memory");
-  if constexpr (POL == 5) asm volatile("global_load_dwordx4 %0, %1, off sc0" : "=v"(v) : "v"(addr) : "memory");
-  return v;
-}
-
-template <int LP, int SP>
-__global__ __launch_bounds__(256) void r1_pol(const RowsArgs<2, 12, 4, true> a) {
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (gid >= a.total) return;
-  const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * 16;
-  u32x4 v[16];
-#pragma unroll
-  for (int m = 0; m < 12; ++m) v[m] = ld_pol<LP>(row_addr(a.msrc[m], stripe, off));
-#pragma unroll
-  for (int x = 0; x < 4; ++x) v[12 + x] = ld_pol<LP>(row_addr(a.xsrc[x], stripe, off));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  u32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
-#pragma unroll
-  for (int m = 0; m < 12; ++m) s0 ^= v[m];
-#pragma unroll
-  for (int x = 0; x < 4; ++x) s1 ^= v[12 + x];
-  st_pol<SP>(row_addr(a.dst[0], stripe, off), s0);
-  st_pol<SP>(row_addr(a.dst[1], stripe, off), s1 ^ s0);
-}
-
-template <int LP, int SP>
-__global__ __launch_bounds__(256) void enc_pol(const PairArgs<4, 12, true> a) {
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (gid >= a.total) return;
-  const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * 16;
-  u32x4 va[12], vb[12];
-#pragma unroll
-  for (int c = 0; c < 12; ++c) {
-    const uint64_t s = row_addr(a.src[c], stripe, off);
-    va[c] = ld_pol<LP>(s);
-    vb[c] = ld_pol<LP>(s + a.half);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  u32x4 sa = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
-#pragma unroll
-  for (int c = 0; c < 12; ++c) {
-    sa ^= va[c];
-    sb ^= vb[c];
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const uint64_t d = row_addr(a.dst[r], stripe, off);
-    st_pol<SP>(d, sa + r);
-    st_pol<SP>(d + a.half, sb + r);
-  }
-}
-
 // Grid-stride XOR-only probes (memory ceiling with a persistent-style grid).
 __global__ __launch_bounds__(256) void r1_xor_gs(const RowsArgs<2, 12, 4, true> a) {
   for (uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; gid < a.total;
@@ -831,27 +758,6 @@ int main(int argc, char** argv) {
       t[5].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
       t[6].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, false>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
       t[7].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<false, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
-    }
-    if (argc > 2 && std::string(argv[2]) == "pol") {
-      std::vector<double> tp[2][12];
-      const char* pn[12] = {"ld nt / st nt", "ld nt / st none", "ld nt / st sc1", "ld nt / st sc0sc1",
-                            "ld nt / st sc0sc1nt", "ld nt / st sc0", "ld none / st nt", "ld sc1 / st nt",
-                            "ld sc0sc1 / st nt", "ld sc0sc1nt / st nt", "ld sc0 / st nt", "ld sc0sc1nt / st sc0sc1nt"};
-#define POLRUN(i, L, S)                                                                              \
-  tp[0][i].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_pol<L, S>), dim3(bl1), dim3(256), 0, 0, ra); }, 5)); \
-  tp[1][i].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_pol<L, S>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
-      for (int round = 0; round < 5; ++round) {
-        POLRUN(0, 1, 1) POLRUN(1, 1, 0) POLRUN(2, 1, 2) POLRUN(3, 1, 3) POLRUN(4, 1, 4) POLRUN(5, 1, 5)
-        POLRUN(6, 0, 1) POLRUN(7, 2, 1) POLRUN(8, 3, 1) POLRUN(9, 4, 1) POLRUN(10, 5, 1) POLRUN(11, 4, 4)
-      }
-      for (int i = 0; i < 12; ++i)
-        for (int k = 0; k < 2; ++k) {
-          std::sort(tp[k][i].begin(), tp[k][i].end());
-          char name[96];
-          std::snprintf(name, sizeof name, "%s xor %s", k ? "enc" : "r1 ", pn[i]);
-          report(name, tp[k][i][2], k ? 16.0 * S2 * n2 : 9.0 * S1 * n1);
-        }
-      return 0;
     }
     const char* nm[8] = {"r1 product", "r1 read+write (xor)", "r1 read only (16 rows)", "r1 write only (2 rows)",
                          "enc product", "enc read+write (xor)", "enc read only (24 halves)", "enc write only (8 halves)"};

@@ -297,6 +297,63 @@ __global__ __launch_bounds__(256) void enc_rw(const PairArgs<4, 12, true> a, uin
   }
 }
 
+// s_setprio probes: the product Encode / ReconstOne bodies with the wave's
+// priority raised while it issues its loads (PR), dropped for the compute.
+template <int PR>
+__global__ __launch_bounds__(256) void enc_prio(const PairArgs<4, 12, true> a) {
+  constexpr int P = 4, C = 12, W = 4;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  uint32_t acc_a[P][W] = {}, acc_b[P][W] = {};
+  uint32_t xa[C][W], xb[C][W];
+  if (PR) __builtin_amdgcn_s_setprio(PR);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const uint64_t s = row_addr(a.src[c], stripe, off);
+    ld<true>(xa[c], s, 16);
+    ld<true>(xb[c], s + a.half, 16);
+  }
+  if (PR) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int c = 0; c + 1 < C; c += 2)
+    pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const uint64_t d = row_addr(a.dst[r], stripe, off);
+    st<true>(acc_a[r], d, 16);
+    st<true>(acc_b[r], d + a.half, 16);
+  }
+}
+
+template <int PR>
+__global__ __launch_bounds__(256) void r1_prio(const RowsArgs<2, 12, 4, true> a) {
+  constexpr int R = 2, NM = 12, NX = 4, W = 4;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * 16;
+  uint32_t acc[R][W] = {};
+  uint32_t xm[NM][W], xx[NX][W];
+  if (PR) __builtin_amdgcn_s_setprio(PR);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) ld<true>(xm[m], row_addr(a.msrc[m], stripe, off), 16);
+#pragma unroll
+  for (int x = 0; x < NX; ++x) ld<true>(xx[x], row_addr(a.xsrc[x], stripe, off), 16);
+  if (PR) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int m = 0; m + 1 < NM; m += 2) rows_mac2<R, W>(acc, a.tab[m], a.tab[m + 1], xm[m], xm[m + 1]);
+#pragma unroll
+  for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
+#pragma unroll
+  for (int r = 0; r < R; ++r) st<true>(acc[r], row_addr(a.dst[r], stripe, off), 16);
+}
+
 // Grid-stride XOR-only probes (memory ceiling with a persistent-style grid).
 __global__ __launch_bounds__(256) void r1_xor_gs(const RowsArgs<2, 12, 4, true> a) {
   for (uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; gid < a.total;
@@ -758,6 +815,28 @@ int main(int argc, char** argv) {
       t[5].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
       t[6].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<true, false>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
       t[7].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_rw<false, true>), dim3(bl2), dim3(256), 0, 0, pa, sink); }, 5));
+    }
+    if (argc > 2 && std::string(argv[2]) == "prio") {
+      std::vector<double> tq[2][4];
+      for (int round = 0; round < 7; ++round) {
+        tq[0][0].push_back(tm.ms([&] { hipLaunchKernelGGL((rows_kernel<2, 12, 4, false, true>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+        tq[0][1].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_prio<0>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+        tq[0][2].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_prio<1>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+        tq[0][3].push_back(tm.ms([&] { hipLaunchKernelGGL((r1_prio<3>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));
+        tq[1][0].push_back(tm.ms([&] { hipLaunchKernelGGL((pair_kernel<4, 12, false, true>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+        tq[1][1].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_prio<0>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+        tq[1][2].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_prio<1>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+        tq[1][3].push_back(tm.ms([&] { hipLaunchKernelGGL((enc_prio<3>), dim3(bl2), dim3(256), 0, 0, pa); }, 5));
+      }
+      const char* qn[4] = {"product", "copy, no setprio", "setprio 1 around loads", "setprio 3 around loads"};
+      for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < 4; ++i) {
+          std::sort(tq[k][i].begin(), tq[k][i].end());
+          char name[96];
+          std::snprintf(name, sizeof name, "%s %s", k ? "enc" : "r1 ", qn[i]);
+          report(name, tq[k][i][3], k ? 16.0 * S2 * n2 : 9.0 * S1 * n1);
+        }
+      return 0;
     }
     const char* nm[8] = {"r1 product", "r1 read+write (xor)", "r1 read only (16 rows)", "r1 write only (2 rows)",
                          "enc product", "enc read+write (xor)", "enc read only (24 halves)", "enc write only (8 halves)"};

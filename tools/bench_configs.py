@@ -100,6 +100,21 @@ def main():
                 secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has, need, s))
                 emit(f"reconst_{lost}", size, n, secs, n * (D + lost) * size, sh)
             del t
+    if "others" in cases:  # other (d, p): runtime-count kernels
+        for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3)):
+            xo = xrs_amd.XRS(d, p)
+            for size in (4096, 1 << 20):
+                n = (4 << 30) // ((d + p) * size)
+                shard, stripe = xrs_amd.batch_strides(size, d + p)
+                t = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device=dev)
+                secs = timed(lambda i: xo.encode_batched(t.data_ptr(), size, shard, stripe, n, s))
+                emit(f"encode_{d}+{p}", size, n, secs, n * (d + p) * size, shard)
+                a_need, _ = xo.get_need_vects(0)
+                secs = timed(lambda i: xo.reconst_one_batched(t.data_ptr(), size, shard, stripe, n,
+                                                              0, s))
+                emit(f"reconst_one_{d}+{p}", size, n, secs,
+                     n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
+                del t
     torch.cuda.empty_cache()
 
 

@@ -39,6 +39,8 @@ struct xrs_codec {
   mutable std::mutex mu;
   mutable uint8_t* staging = nullptr;
   mutable size_t staging_cap = 0;
+  mutable uint8_t* hstaging = nullptr;  // pinned host mirror of `staging` (small stripes)
+  mutable size_t hstaging_cap = 0;
   mutable hipStream_t stream = nullptr;
 
   // host-resident pipeline state (lazy; guarded by pipe_mu): kPipe device
@@ -577,6 +579,23 @@ int ensure_staging(const xrs_codec* x, size_t bytes) {
   return XRS_OK;
 }
 
+// Small stripes go through a pinned host mirror of the device staging: the
+// caller's vects are gathered by CPU memcpy, then ONE H2D, the kernel and ONE
+// D2H (instead of one small copy per vect, each a few microseconds).
+constexpr size_t kPinnedStageMax = 8u << 20;
+
+int ensure_hstaging(const xrs_codec* x, size_t bytes) {
+  if (bytes > x->hstaging_cap) {
+    if (x->hstaging) (void)hipHostFree(x->hstaging);
+    x->hstaging = nullptr;
+    x->hstaging_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1 << 20);
+    if (hipHostMalloc(&x->hstaging, cap, hipHostMallocDefault) != hipSuccess) return XRS_ERR_HIP;
+    x->hstaging_cap = cap;
+  }
+  return XRS_OK;
+}
+
 int h2d(const xrs_codec* x, size_t off, const void* src, size_t n) {
   if (n == 0) return XRS_OK;
   if (!src) return XRS_ERR_INVALID_ARG;
@@ -777,6 +796,7 @@ void xrs_free(xrs_codec* x) {
     DeviceGuard g(x->device);
     if (x->stream) (void)hipStreamDestroy(x->stream);
     if (x->staging) (void)hipFree(x->staging);
+    if (x->hstaging) (void)hipHostFree(x->hstaging);
     for (int i = 0; i < xrs_codec::kPipe; ++i) {
       if (x->pstream[i]) (void)hipStreamDestroy(x->pstream[i]);
       if (x->slot[i]) (void)hipFree(x->slot[i]);
@@ -1061,9 +1081,25 @@ int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
   if (size == 0) return XRS_OK;
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  if ((e = ensure_staging(x, static_cast<size_t>(n) * size))) return e;
+  const size_t total = static_cast<size_t>(n) * size, dbytes = static_cast<size_t>(x->d) * size;
+  if ((e = ensure_staging(x, total))) return e;
+  const Layout L{x->staging, size, total};
+  if (total <= kPinnedStageMax) {
+    if ((e = ensure_hstaging(x, total))) return e;
+    for (int j = 0; j < x->d; ++j) std::memcpy(x->hstaging + static_cast<size_t>(j) * size, vects[j], size);
+    e = hip_err(hipMemcpyAsync(x->staging, x->hstaging, dbytes, hipMemcpyHostToDevice, x->stream));
+    if (!e) e = encode_impl(x, L, size, 1, x->stream);
+    if (!e)
+      e = hip_err(hipMemcpyAsync(x->hstaging + dbytes, x->staging + dbytes, total - dbytes,
+                                 hipMemcpyDeviceToHost, x->stream));
+    const int es = sync(x);
+    if (e || es) return e ? e : es;
+    for (int r = 0; r < x->p; ++r)
+      std::memcpy(vects[x->d + r], x->hstaging + dbytes + static_cast<size_t>(r) * size, size);
+    return XRS_OK;
+  }
   for (int j = 0; j < x->d && !e; ++j) e = h2d(x, static_cast<size_t>(j) * size, vects[j], size);
-  if (!e) e = encode_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size, 1, x->stream);
+  if (!e) e = encode_impl(x, L, size, 1, x->stream);
   for (int r = 0; r < x->p && !e; ++r)
     e = d2h(x, vects[x->d + r], static_cast<size_t>(x->d + r) * size, size);
   const int es = sync(x);
@@ -1092,12 +1128,32 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
   if (!vects[k]) return XRS_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  if ((e = ensure_staging(x, static_cast<size_t>(n) * size))) return e;
+  const size_t total = static_cast<size_t>(n) * size;
+  if ((e = ensure_staging(x, total))) return e;
+  const Layout L{x->staging, size, total};
+  if (total <= kPinnedStageMax) {
+    // Gather the need-set halves into the pinned mirror at their device
+    // offsets; bytes the kernel does not read travel as don't-care.
+    if ((e = ensure_hstaging(x, total))) return e;
+    for (auto& r : reads)
+      std::memcpy(x->hstaging + static_cast<size_t>(r.first) * size + r.second * half,
+                  vects[r.first] + r.second * half, half);
+    e = hip_err(hipMemcpyAsync(x->staging, x->hstaging, total, hipMemcpyHostToDevice, x->stream));
+    if (!e) e = reconst_one_impl(x, L, size, 1, k, x->stream);
+    const size_t ko = static_cast<size_t>(k) * size;
+    if (!e)
+      e = hip_err(hipMemcpyAsync(x->hstaging + ko, x->staging + ko, size, hipMemcpyDeviceToHost,
+                                 x->stream));
+    const int es = sync(x);
+    if (e || es) return e ? e : es;
+    std::memcpy(vects[k], x->hstaging + ko, size);
+    return XRS_OK;
+  }
   for (size_t i = 0; i < reads.size() && !e; ++i) {
     const size_t off = static_cast<size_t>(reads[i].first) * size + reads[i].second * half;
     e = h2d(x, off, vects[reads[i].first] + reads[i].second * half, half);
   }
-  if (!e) e = reconst_one_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size, 1, k, x->stream);
+  if (!e) e = reconst_one_impl(x, L, size, 1, k, x->stream);
   if (!e) e = d2h(x, vects[k], static_cast<size_t>(k) * size, size);
   const int es = sync(x);
   return e ? e : es;

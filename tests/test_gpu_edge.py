@@ -81,18 +81,18 @@ def test_cpp_port_under_host_asan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.fixture(params=["fused", "stepwise"])
+@pytest.fixture(params=["staged", "stepwise"])
 def reconst_mode(request, monkeypatch):
-    if request.param == "fused":
-        monkeypatch.setenv("XRS_RECONST_FUSED", "1")
+    if request.param == "staged":
+        monkeypatch.delenv("XRS_RECONST", raising=False)
     else:
-        monkeypatch.delenv("XRS_RECONST_FUSED", raising=False)
+        monkeypatch.setenv("XRS_RECONST", "steps")
     return request.param
 
 
 @pytest.mark.parametrize("size", [2, 4096, 1030])
 def test_reconst_random_both_paths(rng, reconst_mode, size):
-    """General Reconst through the fused one-pass plan and the step-by-step
+    """General Reconst through the staged one-pass kernel and the step-by-step
     plan: identical buffers (side effects included) to the oracle."""
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
     for _ in range(60):
@@ -130,3 +130,27 @@ def test_reconst_other_configs_both_paths(rng, reconst_mode, d, p):
         o.reconst(b, has, need)
         for i in range(d + p):
             assert np.array_equal(a[i], b[i]), (reconst_mode, d, p, lost, need, i)
+
+
+@pytest.mark.parametrize("order", ["sorted", "reversed"])
+def test_reconst_every_loss_pattern(rng, order):
+    """Every loss set of 1..p shards of a 12+4 stripe (2,516 patterns), need =
+    the lost set, survivors sorted or reversed (reversed makes the first d
+    survivors parity-heavy, so the staged kernel reads extra a-rows): buffers
+    identical to the oracle, side effects included."""
+    from itertools import combinations
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    base = stripe(rng, 64)
+    for k in range(1, P + 1):
+        for lost in combinations(range(D + P), k):
+            has = [i for i in range(D + P) if i not in lost]
+            if order == "reversed":
+                has = has[::-1]
+            a = [r.copy() for r in base]
+            for t in lost:
+                a[t][:] = 0xA5
+            b = [r.copy() for r in a]
+            x.reconst(a, has, list(lost))
+            o.reconst(b, has, list(lost))
+            for i in range(D + P):
+                assert np.array_equal(a[i], b[i]), (lost, order, i)

@@ -94,11 +94,15 @@ def main():
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)
-            for lost in (2, 3, 4):
-                need = list(range(lost))
-                has = list(range(lost, D + P))
-                secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has, need, s))
-                emit(f"reconst_{lost}", size, n, secs, n * (D + lost) * size, sh)
+            for mode in ("staged", "steps"):
+                os.environ["XRS_RECONST"] = mode  # read per call by the library
+                for lost in (1, 2, 3, 4):
+                    need = list(range(lost))
+                    has = list(range(lost, D + P))
+                    secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has,
+                                                             need, s))
+                    emit(f"reconst_{lost}_{mode}", size, n, secs, n * (D + lost) * size, sh)
+            os.environ.pop("XRS_RECONST", None)
             del t
     if "others" in cases:  # other (d, p): runtime-count kernels
         for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3)):

@@ -276,108 +276,100 @@ int reconst_one_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_
   return run_rows(dst, ms, xs, false, half, n_stripes, s);
 }
 
-// General Reconst (xrs.go:236-301) composed into ONE mix-kernel pass.  Every
-// value the reference's four steps write is linear in the survivors' halves:
-//   a_t  (t not in dpHas)         = sum_m A[t][m] a(has_m)                 step 1
-//   b'_h (surviving parity h > d) = b_h ^ XOR_{j in XS[h]} abar_j          step 2
-//   b_t  (t in need)              = sum_m B[t][m] rsb(has_m)               step 3
-//                                   ^ [t > d] XOR_{j in XS[t]} abar_j      step 4
-// with abar_j = a_j if j survives, else its step-1 row, and rsb(h) = b'_h for
-// a retrieved parity, b_h otherwise.  A repeated index toggles like the
-// reference's loops.  Returns 1 (not handled) when the plan does not fit
-// (more than kMixOut outputs or kMixSrc source shards); the caller then runs
-// the step-by-step path.  Inputs were validated by the caller.
-int reconst_fused(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes,
-                  const int* dp_has, int n_has, const std::vector<int>& a_lost,
-                  const std::vector<std::vector<uint8_t>>& acoef, const std::vector<int>& uniq,
-                  const std::vector<int>& rep, const std::vector<std::vector<uint8_t>>& bcoef,
-                  hipStream_t s, Written* w) {
-  const int d = x->d, p = x->p, n = d + p;
-  const GF& gf = GF::get();
+// General Reconst (xrs.go:236-301) as ONE staged-kernel pass (xrs_plan.h
+// StagedPlan): stage 1 rebuilds the lost a-halves, stage 2 is retrieveRS on
+// the surviving piggybacked parity, stage 3+4 rebuild the needed b-halves and
+// re-piggyback them, all from registers.  Applies when the call is "clean":
+// every index valid and distinct, need disjoint from dpHas, both inverses
+// exist, and the plan fits kStSrc/kStOut.  Otherwise returns 1 and the caller
+// runs the step-by-step plan, which reproduces the reference's partial side
+// effects on errors and its toggling on repeated indexes.
+int reconst_staged(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes,
+                   const int* dp_has, int n_has, const int* need, int n_need, hipStream_t s,
+                   Written* w) {
+  const int d = x->d, n = x->d + x->p;
+  if (d > xrs::kStSrc || n_has < d || n_need > xrs::kStOut) return 1;
+  std::vector<int> in_has(n, 0), lost_q(n, -1), apos(n, -1), bpos(n, -1);
+  for (int i = 0; i < n_has; ++i) {
+    if (dp_has[i] < 0 || dp_has[i] >= n || in_has[dp_has[i]]) return 1;
+    in_has[dp_has[i]] = 1;
+  }
+  std::vector<int> seen(n, 0);
+  for (int u = 0; u < n_need; ++u) {
+    if (need[u] < 0 || need[u] >= n || in_has[need[u]] || seen[need[u]]) return 1;
+    seen[need[u]] = 1;
+  }
+  std::vector<int> a_lost;
+  for (int i = 0; i < n; ++i)
+    if (!in_has[i]) a_lost.push_back(i);
+  if (static_cast<int>(a_lost.size()) > xrs::kStOut) return 1;
+  std::vector<std::vector<uint8_t>> acoef, bcoef;
+  if (survivor_rows(x, dp_has, n_has, a_lost, &acoef) != XRS_OK) return 1;
+  const std::vector<int> outs(need, need + n_need);
+  if (survivor_rows(x, dp_has, n_has, outs, &bcoef) != XRS_OK) return 1;
+  for (size_t q = 0; q < a_lost.size(); ++q) lost_q[a_lost[q]] = static_cast<int>(q);
+
+  xrs::StagedPlan plan;
+  std::memset(&plan, 0, sizeof(plan));
   const size_t half = size / 2;
-  std::vector<int> in_has(n, 0), lost_row(n, -1), retrieved(n, 0);
-  for (int i = 0; i < n_has; ++i)
-    if (dp_has[i] >= 0 && dp_has[i] < n) in_has[dp_has[i]] = 1;
-  for (size_t q = 0; q < a_lost.size(); ++q) lost_row[a_lost[q]] = static_cast<int>(q);
-  for (int i = 0; i < n_has; ++i)
-    if (dp_has[i] > d && dp_has[i] < n) retrieved[dp_has[i]] ^= 1;
-  for (int h = 0; h < n; ++h)
-    if (x->xs[h].empty()) retrieved[h] = 0;
-  // outputs: (shard, half) with coefficient rows over shards (a and b)
-  struct Out {
-    int shard, h;
-    std::vector<uint8_t> ca, cb;
-  };
-  std::vector<Out> outs;
-  auto add_abar = [&](std::vector<uint8_t>& ca, int j, uint8_t coef) {
-    if (coef == 0) return;
-    if (in_has[j]) {
-      ca[j] ^= coef;
-    } else {
-      const auto& row = acoef[lost_row[j]];
-      for (int m = 0; m < d; ++m) ca[dp_has[m]] ^= gf.mul(coef, row[m]);
-    }
-  };
-  for (size_t q = 0; q < a_lost.size(); ++q) {
-    Out o{a_lost[q], 0, std::vector<uint8_t>(n, 0), std::vector<uint8_t>(n, 0)};
-    for (int m = 0; m < d; ++m) o.ca[dp_has[m]] ^= acoef[q][m];
-    outs.push_back(std::move(o));
+  plan.nd = d;
+  for (int m = 0; m < d; ++m) {
+    plan.asrc[m] = L.row(dp_has[m], 0);
+    plan.bsrc[m] = L.row(dp_has[m], half);
+    apos[dp_has[m]] = bpos[dp_has[m]] = m;
   }
-  std::vector<int> is_need(n, 0);
-  for (int t : uniq) is_need[t] = 1;
-  for (int h = d + 1; h < n; ++h) {
-    if (!retrieved[h] || is_need[h]) continue;  // a needed h is rewritten by step 3/4
-    Out o{h, 1, std::vector<uint8_t>(n, 0), std::vector<uint8_t>(n, 0)};
-    o.cb[h] ^= 1;
-    for (int j : x->xs[h]) add_abar(o.ca, j, 1);
-    outs.push_back(std::move(o));
-  }
-  for (size_t u = 0; u < uniq.size(); ++u) {
-    const int t = uniq[u];
-    Out o{t, 1, std::vector<uint8_t>(n, 0), std::vector<uint8_t>(n, 0)};
-    for (int m = 0; m < d; ++m) {
-      const int hm = dp_has[m];
-      const uint8_t c = bcoef[u][m];
-      o.cb[hm] ^= c;
-      if (retrieved[hm])
-        for (int j : x->xs[hm]) add_abar(o.ca, j, c);
-    }
-    if (t > d && (rep[u] & 1))
-      for (int j : x->xs[t]) add_abar(o.ca, j, 1);
-    outs.push_back(std::move(o));
-  }
-  if (outs.empty()) return XRS_OK;
-  // source shards: every shard with a nonzero coefficient
-  std::vector<int> src;
-  std::vector<uint8_t> use(n, 0);
-  for (const Out& o : outs)
-    for (int j = 0; j < n; ++j) use[j] |= (o.ca[j] ? 1 : 0) | (o.cb[j] ? 2 : 0);
-  for (int j = 0; j < n; ++j)
-    if (use[j]) src.push_back(j);
-  if (static_cast<int>(outs.size()) > xrs::kMixOut || static_cast<int>(src.size()) > xrs::kMixSrc ||
-      src.empty())
-    return 1;
-  if (half > 0 && n_stripes > 0) {
-    xrs::MixPlan plan;
-    std::memset(&plan, 0, sizeof(plan));
-    plan.n_out = static_cast<int>(outs.size());
-    plan.n_src = static_cast<int>(src.size());
-    plan.half = half;
-    plan.n_stripes = n_stripes;
-    for (size_t c = 0; c < src.size(); ++c) {
-      plan.src[c] = L.row(src[c], 0);
-      plan.use[c] = use[src[c]];
-    }
-    for (size_t r = 0; r < outs.size(); ++r) {
-      plan.dst[r] = L.row(outs[r].shard, outs[r].h ? half : 0);
-      for (size_t c = 0; c < src.size(); ++c) {
-        plan.ca[r][c] = outs[r].ca[src[c]];
-        plan.cb[r][c] = outs[r].cb[src[c]];
+  plan.na = plan.nb = d;
+  bool fits = true;
+  // abar(XS[h]): surviving members from their a-rows (extra rows appended),
+  // lost members from the stage-1 registers.
+  auto abar = [&](int h) {
+    uint32_t mask = 0;
+    for (int j : x->xs[h]) {
+      if (!in_has[j]) {
+        mask ^= 1u << (xrs::kStSrc + lost_q[j]);
+        continue;
       }
+      if (apos[j] < 0) {
+        if (plan.na == xrs::kStSrc) {
+          fits = false;
+          continue;
+        }
+        apos[j] = plan.na;
+        plan.asrc[plan.na++] = L.row(j, 0);
+      }
+      mask ^= 1u << apos[j];
     }
-    if (xrs::launch_mix(plan, s) != 0) return XRS_ERR_HIP;
+    return mask;
+  };
+  plan.nl = static_cast<int>(a_lost.size());
+  for (int q = 0; q < plan.nl; ++q) {
+    plan.adst[q] = L.row(a_lost[q], 0);
+    for (int m = 0; m < d; ++m) plan.acoef[m][q] = acoef[q][m];
   }
-  for (const Out& o : outs) w->add(o.shard, o.h);
+  for (int h = d + 1; h < n; ++h) {  // xrs.go:305-320: h in dpHas, h > d
+    if (!in_has[h] || x->xs[h].empty()) continue;
+    if (bpos[h] < 0) {
+      if (plan.nb == xrs::kStSrc) return 1;
+      bpos[h] = plan.nb;
+      plan.bsrc[plan.nb++] = L.row(h, half);
+    }
+    plan.bret[bpos[h]] = abar(h);
+    plan.bstore |= 1u << bpos[h];
+  }
+  plan.nn = n_need;
+  for (int u = 0; u < n_need; ++u) {
+    plan.bdst[u] = L.row(need[u], half);
+    for (int m = 0; m < d; ++m) plan.bcoef[m][u] = bcoef[u][m];
+    if (need[u] > d) plan.nmask[u] = abar(need[u]);  // xrs.go:283-297
+  }
+  if (!fits) return 1;
+  plan.half = half;
+  plan.n_stripes = n_stripes;
+  if (half > 0 && n_stripes > 0 && xrs::launch_staged(plan, s) != 0) return XRS_ERR_HIP;
+  for (int t : a_lost) w->add(t, 0);
+  for (int h = d + 1; h < n; ++h)
+    if (in_has[h] && !x->xs[h].empty()) w->add(h, 1);
+  for (int u = 0; u < n_need; ++u) w->add(need[u], 1);
   return XRS_OK;
 }
 
@@ -387,38 +379,12 @@ int reconst_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stri
                  Written* w) {
   const int d = x->d, p = x->p;
   const size_t half = size / 2;
-  // XRS_RECONST_FUSED=1: one composed mix-kernel pass (when every step
-  // validates and the plan fits).  Measured slower than the step-by-step
-  // plan on 12+4 (expanding each lost a-half into every output that uses it
-  // triples the GF work; profiles/r01_bench_multi.log), so it is opt-in;
-  // tests run both paths.
-  const char* fz = std::getenv("XRS_RECONST_FUSED");
-  if (fz && fz[0] == '1') {
-    std::vector<int> a_lost;
-    for (int i = 0; i < d + p; ++i)
-      if (std::find(dp_has, dp_has + n_has, i) == dp_has + n_has) a_lost.push_back(i);
-    std::vector<std::vector<uint8_t>> acoef, bcoef;
-    std::vector<int> outs(need, need + n_need);
-    if (survivor_rows(x, dp_has, n_has, a_lost, &acoef) == XRS_OK &&
-        survivor_rows(x, dp_has, n_has, outs, &bcoef) == XRS_OK) {
-      std::vector<int> uniq, rep;
-      std::vector<size_t> qidx;
-      for (int q = 0; q < n_need; ++q) {
-        auto it = std::find(uniq.begin(), uniq.end(), need[q]);
-        if (it == uniq.end()) {
-          uniq.push_back(need[q]);
-          rep.push_back(1);
-          qidx.push_back(q);
-        } else {
-          rep[it - uniq.begin()]++;
-        }
-      }
-      std::vector<std::vector<uint8_t>> bu;
-      for (size_t u = 0; u < uniq.size(); ++u) bu.push_back(bcoef.empty() ? std::vector<uint8_t>() : bcoef[qidx[u]]);
-      const int e = reconst_fused(x, L, size, n_stripes, dp_has, n_has, a_lost, acoef, uniq, rep,
-                                  bu, s, w);
-      if (e <= 0) return e;  // handled (or failed); 1 = fall through
-    }
+  // One staged pass when the call is clean; XRS_RECONST=steps forces the
+  // step-by-step plan (tests run both).
+  const char* mode = std::getenv("XRS_RECONST");
+  if (!(mode && std::strcmp(mode, "steps") == 0)) {
+    const int e = reconst_staged(x, L, size, n_stripes, dp_has, n_has, need, n_need, s, w);
+    if (e <= 0) return e;  // handled (or failed); 1 = not applicable
   }
   // Step 1: a-halves of every vect not in dpHas (xrs.go:247-262).
   std::vector<int> a_lost;

@@ -23,8 +23,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
-#include <map>
-#include <mutex>
 
 #include "gf256.h"
 #include "xrs_plan.h"
@@ -350,132 +348,157 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
   for (int r = 0; r < R; ++r) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
 }
 
-// ============================================================ mix kernel
-// General Reconst in one pass: out_r = sum_c ca[r][c]*a_c ^ cb[r][c]*b_c.
-// Sources are read once each (only the halves `use` asks for); zero
-// coefficients are skipped with wave-uniform branches, 1 is a plain XOR.
-struct MixArgs {
-  RowRef src[kMixSrc];
-  uint32_t use[kMixSrc];
-  RowRef dst[kMixOut];
-  uint8_t ca[kMixOut][kMixSrc];
-  uint8_t cb[kMixOut][kMixSrc];
-  const GfTab* tabs;  // device table, tabs[c] = GfTab of coefficient c
-  int n_out, n_src;
+// ============================================================ staged kernel
+// General Reconst in one pass (xrs_plan.h StagedPlan): lost a-halves are
+// rebuilt once and feed the retrieveRS and re-piggyback XORs from registers;
+// survivors' b-halves are returned to RS form in registers, written back (the
+// reference's side effect) and feed the b-half rebuild.  Every row is read
+// once and every written row is written once.
+template <int NL, int NN, bool VEC>
+struct StagedArgs {
+  GfTab at[kStSrc][NL > 0 ? NL : 1];
+  GfTab bt[kStSrc][NN > 0 ? NN : 1];
+  RowRef asrc[kStSrc], bsrc[kStSrc];
+  RowRef adst[kStOut], bdst[kStOut];
+  uint32_t bret[kStSrc];
+  uint32_t nmask[kStOut];
+  uint32_t bstore;
+  int nd, na, nb, nl, nn;
   uint64_t half, chunks, total;
 };
 
-template <int R, int W>
-__device__ __forceinline__ void mix_term(uint32_t (&acc)[R][W], int r, uint32_t k,
-                                         const GfTab* tabs, const uint32_t* x, const Sel* s) {
-  if (k == 0) return;
-  if (k == 1) {
+// acc ^= abar(mask): wave-uniform branches, the masks have few bits set.
+template <int NL, int W>
+__device__ __forceinline__ void abar_xor(uint32_t* acc, uint32_t mask, const uint32_t (&xa)[kStSrc][W],
+                                         const uint32_t (&al)[NL > 0 ? NL : 1][W]) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) acc[r][w] ^= x[w];
-    return;
-  }
-  const GfTab t = tabs[k];
+  for (int j = 0; j < kStSrc; ++j)
+    if ((mask >> j) & 1u)
 #pragma unroll
-  for (int w = 0; w < W; ++w) acc[r][w] ^= gmul(t, s[w]);
+      for (int w = 0; w < W; ++w) acc[w] ^= xa[j][w];
+#pragma unroll
+  for (int q = 0; q < NL; ++q)
+    if ((mask >> (kStSrc + q)) & 1u)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[w] ^= al[q][w];
 }
 
-template <int R, bool VEC>
-__global__ __launch_bounds__(kBlock) void mix_kernel(const MixArgs a) {
+template <int NL, int NN, bool VEC>
+__global__ __launch_bounds__(kBlock) void staged_kernel(const StagedArgs<NL, NN, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
+  constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
-  uint32_t acc[R][W];
+
+  uint32_t xa[kStSrc][W], xb[kStSrc][W];
+  __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int r = 0; r < R; ++r)
+  for (int m = 0; m < kStSrc; ++m)
+    if (m < a.na) ld<VEC>(xa[m], row_addr(a.asrc[m], stripe, off), nb);
 #pragma unroll
-    for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-  for (int c = 0; c < a.n_src; ++c) {
-    const uint64_t s = row_addr(a.src[c], stripe, off);
-    const uint32_t use = a.use[c];
-    uint32_t xa[W], xb[W];
-    Sel sa[W], sb[W];
-    if (use & 1u) {
-      ld<VEC>(xa, s, nb);
+  for (int m = 0; m < kStSrc; ++m)
+    if (m < a.nb) ld<VEC>(xb[m], row_addr(a.bsrc[m], stripe, off), nb);
+  __builtin_amdgcn_s_setprio(0);
+
+  // Stage 1: lost a-halves (xrs.go:247-262).
+  uint32_t al[L1][W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) sa[w] = sel_of(xa[w]);
+  for (int q = 0; q < L1; ++q)
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (r < a.n_out) mix_term<R, W>(acc, r, a.ca[r][c], a.tabs, xa, sa);
+    for (int w = 0; w < W; ++w) al[q][w] = 0u;
+  if constexpr (NL > 0) {
+#pragma unroll
+    for (int m = 0; m < kStSrc; m += 2) {
+      if (m + 1 < a.nd) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+      else if (m < a.nd) rows_mac1<NL, W>(al, a.at[m], xa[m]);
     }
-    if (use & 2u) {
-      ld<VEC>(xb, s + a.half, nb);
 #pragma unroll
-      for (int w = 0; w < W; ++w) sb[w] = sel_of(xb[w]);
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (r < a.n_out) mix_term<R, W>(acc, r, a.cb[r][c], a.tabs, xb, sb);
-    }
+    for (int q = 0; q < NL; ++q)
+      if (q < a.nl) st<VEC>(al[q], row_addr(a.adst[q], stripe, off), nb);
   }
+
+  // Stage 2: retrieveRS on surviving piggybacked parity (xrs.go:305-320).
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (r < a.n_out) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
+  for (int m = 0; m < kStSrc; ++m)
+    if (m < a.nb && a.bret[m]) {
+      abar_xor<NL, W>(xb[m], a.bret[m], xa, al);
+      if ((a.bstore >> m) & 1u) st<VEC>(xb[m], row_addr(a.bsrc[m], stripe, off), nb);
+    }
+
+  // Stages 3+4: needed b-halves, re-piggybacked (xrs.go:270-298).
+  if constexpr (NN > 0) {
+    uint32_t ob[N1][W];
+#pragma unroll
+    for (int u = 0; u < NN; ++u) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) ob[u][w] = 0u;
+      if (a.nmask[u]) abar_xor<NL, W>(ob[u], a.nmask[u], xa, al);
+    }
+#pragma unroll
+    for (int m = 0; m < kStSrc; m += 2) {
+      if (m + 1 < a.nd) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+      else if (m < a.nd) rows_mac1<NN, W>(ob, a.bt[m], xb[m]);
+    }
+#pragma unroll
+    for (int u = 0; u < NN; ++u)
+      if (u < a.nn) st<VEC>(ob[u], row_addr(a.bdst[u], stripe, off), nb);
+  }
 }
 
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
-// Per-device table of all 256 coefficients for the mix kernel (built once).
-const GfTab* device_tabs() {
-  static std::mutex mu;
-  static std::map<int, GfTab*> cache;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(dev);
-  if (it != cache.end()) return it->second;
-  GfTab host[256];
-  for (int c = 0; c < 256; ++c) host[c] = GF::get().tab(static_cast<uint8_t>(c));
-  GfTab* d = nullptr;
-  if (hipMalloc(&d, sizeof(host)) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(d);
-    return nullptr;
-  }
-  cache[dev] = d;
-  return d;
-}
-
-template <int R, bool VEC>
-int launch_mix_t(const MixPlan& p, const GfTab* tabs, hipStream_t stream) {
-  MixArgs a;
+template <int NL, int NN, bool VEC>
+int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
+  StagedArgs<NL, NN, VEC> a;
   std::memset(&a, 0, sizeof(a));
-  for (int c = 0; c < p.n_src; ++c) {
-    a.src[c] = p.src[c];
-    a.use[c] = p.use[c];
+  const GF& gf = GF::get();
+  for (int m = 0; m < kStSrc; ++m) {
+    for (int q = 0; q < NL; ++q) a.at[m][q] = gf.tab(p.acoef[m][q]);
+    for (int u = 0; u < NN; ++u) a.bt[m][u] = gf.tab(p.bcoef[m][u]);
+    a.asrc[m] = p.asrc[m];
+    a.bsrc[m] = p.bsrc[m];
+    a.bret[m] = p.bret[m];
   }
-  for (int r = 0; r < p.n_out; ++r) {
-    a.dst[r] = p.dst[r];
-    for (int c = 0; c < p.n_src; ++c) {
-      a.ca[r][c] = p.ca[r][c];
-      a.cb[r][c] = p.cb[r][c];
-    }
+  for (int q = 0; q < kStOut; ++q) {
+    a.adst[q] = p.adst[q];
+    a.bdst[q] = p.bdst[q];
+    a.nmask[q] = p.nmask[q];
   }
-  a.tabs = tabs;
-  a.n_out = p.n_out;
-  a.n_src = p.n_src;
+  a.bstore = p.bstore;
+  a.nd = p.nd;
+  a.na = p.na;
+  a.nb = p.nb;
+  a.nl = p.nl;
+  a.nn = p.nn;
   a.half = p.half;
   a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((mix_kernel<R, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
-                     stream, a);
+  hipLaunchKernelGGL((staged_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+                     0, stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
+// Exact-count instantiations for lost-data-only Reconst (nl == nn, the common
+// case); everything else runs the 4/4 kernel with zero padding.
 template <bool VEC>
-int launch_mix_r(const MixPlan& p, const GfTab* tabs, hipStream_t s) {
-  if (p.n_out <= 4) return launch_mix_t<4, VEC>(p, tabs, s);
-  if (p.n_out <= 8) return launch_mix_t<8, VEC>(p, tabs, s);
-  return launch_mix_t<12, VEC>(p, tabs, s);
+int launch_staged_r(const StagedPlan& p, hipStream_t s) {
+  if constexpr (VEC) {
+    if (p.nl == p.nn) {
+      switch (p.nl) {
+        case 1: return launch_staged_t<1, 1, VEC>(p, s);
+        case 2: return launch_staged_t<2, 2, VEC>(p, s);
+        case 3: return launch_staged_t<3, 3, VEC>(p, s);
+        default: break;
+      }
+    }
+  }
+  return launch_staged_t<4, 4, VEC>(p, s);
 }
 
 template <int P, int C, bool ACC, bool VEC>
@@ -577,16 +600,17 @@ int launch_pair(const PairPlan& p, void* stream) {
   return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
 }
 
-int launch_mix(const MixPlan& p, void* stream) {
+int launch_staged(const StagedPlan& p, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.n_out < 1 || p.n_out > kMixOut || p.n_src < 1 || p.n_src > kMixSrc)
+  if (p.nd < 1 || p.nd > p.na || p.nd > p.nb || p.na > kStSrc || p.nb > kStSrc || p.nl < 0 ||
+      p.nl > kStOut || p.nn < 0 || p.nn > kStOut)
     return static_cast<int>(hipErrorInvalidValue);
-  const GfTab* tabs = device_tabs();
-  if (!tabs) return static_cast<int>(hipErrorOutOfMemory);
   bool vec = aligned16(p.half);
-  for (int c = 0; c < p.n_src && vec; ++c) vec = aligned16(p.src[c].ptr) && aligned16(p.src[c].stripe_stride);
-  for (int r = 0; r < p.n_out && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
-  return vec ? launch_mix_r<true>(p, tabs, s) : launch_mix_r<false>(p, tabs, s);
+  for (int m = 0; m < p.na && vec; ++m) vec = aligned16(p.asrc[m].ptr) && aligned16(p.asrc[m].stripe_stride);
+  for (int m = 0; m < p.nb && vec; ++m) vec = aligned16(p.bsrc[m].ptr) && aligned16(p.bsrc[m].stripe_stride);
+  for (int q = 0; q < p.nl && vec; ++q) vec = aligned16(p.adst[q].ptr) && aligned16(p.adst[q].stripe_stride);
+  for (int u = 0; u < p.nn && vec; ++u) vec = aligned16(p.bdst[u].ptr) && aligned16(p.bdst[u].stripe_stride);
+  return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
 }
 
 int launch_rows(const RowsPlan& p, void* stream) {

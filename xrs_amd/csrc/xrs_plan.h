@@ -67,21 +67,27 @@ struct RowsPlan {
   uint64_t n_stripes;
 };
 
-// "mix" kernel: one pass for the whole general Reconst (xrs.go:236-301).
-// Sources are shards (a-half at ptr, b-half at ptr + half); every output is a
-// half-row written as sum_c ca[r][c]*a_c ^ cb[r][c]*b_c (dense, zero-skipped,
-// coefficient 1 is a plain XOR).  Coefficients index a device table of all
-// 256 GfTabs, so the plan itself stays small.
-constexpr int kMixOut = 12;
-constexpr int kMixSrc = 16;
+// "staged" kernel: the general Reconst (xrs.go:236-301) in one pass, each of
+// the reference's four steps kept as a stage in registers:
+//   1. al_q = sum_{m<nd} acoef[m][q] * a(asrc_m)          -> adst_q   (lost a-halves)
+//   2. b(bsrc_m) ^= abar(bret[m]), stored if bstore bit m  (retrieveRS)
+//   3. out_u = sum_{m<nd} bcoef[m][u] * b(bsrc_m)  ^  abar(nmask[u]) -> bdst_u
+// where abar(mask) XORs a-rows (bit m < kStSrc: a(asrc_m)) and rebuilt lost
+// a-halves (bit kStSrc + q: al_q).  asrc/bsrc[0..nd) are the d survivors used
+// by the RS inverse; entries past nd are extra survivors read only for XORs.
+constexpr int kStSrc = 16;
+constexpr int kStOut = 4;
 
-struct MixPlan {
-  int n_out, n_src;
-  RowRef src[kMixSrc];  // shard rows (a-half address)
-  uint8_t use[kMixSrc];  // bit 0: a-half read, bit 1: b-half read
-  RowRef dst[kMixOut];  // output half-rows
-  uint8_t ca[kMixOut][kMixSrc];
-  uint8_t cb[kMixOut][kMixSrc];
+struct StagedPlan {
+  int nd;      // GF sources (d)
+  int na, nb;  // a-/b-half rows read (nd + extras), <= kStSrc
+  int nl, nn;  // lost a-halves / needed b-halves written, <= kStOut
+  RowRef asrc[kStSrc], bsrc[kStSrc];
+  RowRef adst[kStOut], bdst[kStOut];
+  uint8_t acoef[kStSrc][kStOut], bcoef[kStSrc][kStOut];
+  uint32_t bret[kStSrc];   // abar mask XORed into b row m (0: none)
+  uint32_t bstore;         // bit m: write b row m back
+  uint32_t nmask[kStOut];  // abar mask XORed into output u
   uint64_t half;
   uint64_t n_stripes;
 };
@@ -89,6 +95,6 @@ struct MixPlan {
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.
 int launch_pair(const PairPlan& plan, void* stream);
 int launch_rows(const RowsPlan& plan, void* stream);
-int launch_mix(const MixPlan& plan, void* stream);
+int launch_staged(const StagedPlan& plan, void* stream);
 
 }  // namespace xrs

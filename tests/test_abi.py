@@ -110,3 +110,15 @@ def test_compute_without_gpu_fails_loudly():
         x.encode([np.zeros(8, np.uint8) for _ in range(16)])
     with pytest.raises(xrs_amd.XRSError, match="no gpu device"):
         x.encode_batched(1 << 20, 4096, 4096, 65536, 1)
+
+
+def test_single_hip_runtime():
+    """The codec library shares torch's HIP runtime (xrs_amd/__init__.py
+    _load): one libamdhip64 mapped, whichever of the two is imported first."""
+    import subprocess
+    import sys
+    code = ("import xrs_amd, torch; rt = xrs_amd.hip_runtimes(); "
+            "assert len(rt) == 1, rt; print(rt[0])")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]

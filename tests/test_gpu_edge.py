@@ -81,11 +81,13 @@ def test_cpp_port_under_host_asan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.fixture(params=["staged", "stepwise"])
+@pytest.fixture(params=["staged", "staged_early", "stepwise"])
 def reconst_mode(request, monkeypatch):
-    if request.param == "staged":
-        monkeypatch.delenv("XRS_RECONST", raising=False)
-    else:
+    monkeypatch.delenv("XRS_RECONST", raising=False)
+    monkeypatch.delenv("XRS_STAGED_LATE", raising=False)
+    if request.param == "staged_early":
+        monkeypatch.setenv("XRS_STAGED_LATE", "0")
+    elif request.param == "stepwise":
         monkeypatch.setenv("XRS_RECONST", "steps")
     return request.param
 
@@ -133,7 +135,7 @@ def test_reconst_other_configs_both_paths(rng, reconst_mode, d, p):
 
 
 @pytest.mark.parametrize("order", ["sorted", "reversed"])
-def test_reconst_every_loss_pattern(rng, order):
+def test_reconst_every_loss_pattern(rng, reconst_mode, order):
     """Every loss set of 1..p shards of a 12+4 stripe (2,516 patterns), need =
     the lost set, survivors sorted or reversed (reversed makes the first d
     survivors parity-heavy, so the staged kernel reads extra a-rows): buffers
@@ -154,3 +156,32 @@ def test_reconst_every_loss_pattern(rng, order):
             o.reconst(b, has, list(lost))
             for i in range(D + P):
                 assert np.array_equal(a[i], b[i]), (lost, order, i)
+
+
+def test_codec_first_then_torch():
+    """A codec call before torch touches the GPU, then torch: one HIP runtime,
+    torch still sees the device, and a batched call on torch memory works."""
+    import subprocess
+    import sys
+    code = """
+import numpy as np, xrs_amd
+x = xrs_amd.XRS(12, 4)
+v = [np.full(4096, i, np.uint8) for i in range(16)]
+x.encode(v)
+import torch
+assert torch.cuda.is_available()
+assert len(xrs_amd.hip_runtimes()) == 1, xrs_amd.hip_runtimes()
+t = torch.zeros(16 * 4096, dtype=torch.uint8, device="cuda")
+for i in range(12):
+    t[i * 4096:(i + 1) * 4096] = i
+x.encode_batched(t.data_ptr(), 4096, 4096, 16 * 4096, 1, torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize()
+got = t.cpu().numpy().reshape(16, 4096)
+for r in range(12, 16):
+    assert np.array_equal(got[r], v[r]), r
+print("ok")
+"""
+    import os
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

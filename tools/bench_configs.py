@@ -94,8 +94,10 @@ def main():
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)
-            for mode in ("staged", "steps"):
-                os.environ["XRS_RECONST"] = mode  # read per call by the library
+            for mode in ("late", "early", "steps"):
+                # read per call by the library
+                os.environ["XRS_RECONST"] = mode
+                os.environ["XRS_STAGED_LATE"] = "0" if mode == "early" else "1"
                 for lost in (1, 2, 3, 4):
                     need = list(range(lost))
                     has = list(range(lost, D + P))
@@ -103,6 +105,7 @@ def main():
                                                              need, s))
                     emit(f"reconst_{lost}_{mode}", size, n, secs, n * (D + lost) * size, sh)
             os.environ.pop("XRS_RECONST", None)
+            os.environ.pop("XRS_STAGED_LATE", None)
             del t
     if "others" in cases:  # other (d, p): runtime-count kernels
         for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3)):

@@ -16,7 +16,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-__all__ = ["XRS", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides"]
+__all__ = ["XRS", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
@@ -33,12 +33,33 @@ class XRSError(Exception):
         self.code = code
 
 
+def hip_runtimes() -> list:
+    """Distinct libamdhip64 files mapped into this process (should be one)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+    except OSError:
+        return []
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"xrs_amd: {LIB_PATH} is not built (run __graft_entry__.build() or "
             "make -C xrs_amd/csrc); there is no CPU fallback")
+    # One HIP runtime per process.  PyTorch-ROCm bundles its own
+    # libamdhip64 (soname libamdhip64.so.7) and links it by the unversioned
+    # name: loaded first, it also satisfies this library's dependency; loaded
+    # second, the loader would map a second runtime next to /opt/rocm's, and
+    # device pointers, streams and events would belong to different runtimes.
+    # So torch, when installed, is loaded before the codec library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
+    if len(hip_runtimes()) > 1:
+        raise ImportError(f"xrs_amd: two HIP runtimes in this process: {hip_runtimes()}")
     I, Z, P = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
     IP = ctypes.POINTER(ctypes.c_int)
     PP = ctypes.POINTER(ctypes.c_void_p)

@@ -22,6 +22,7 @@
 //    runtime-count variants.  Misaligned / odd sizes take a byte-granular path.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "gf256.h"
@@ -362,8 +363,10 @@ struct StagedArgs {
   RowRef adst[kStOut], bdst[kStOut];
   uint32_t bret[kStSrc];
   uint32_t nmask[kStOut];
+  uint32_t rmask[kStOut];  // the nonzero bret[] entries, compacted (late variant)
+  int rb[kStOut];          // ... and their b-row indexes
   uint32_t bstore;
-  int nd, na, nb, nl, nn;
+  int nd, na, nb, nl, nn, nr;
   uint64_t half, chunks, total;
 };
 
@@ -448,6 +451,80 @@ __global__ __launch_bounds__(kBlock) void staged_kernel(const StagedArgs<NL, NN,
   }
 }
 
+// Late-b variant: the abar XORs are folded into a few accumulators right
+// after stage 1, so the a-rows are dead before the b-rows are loaded (about
+// 110 VGPRs instead of 185: twice the waves per SIMD, half the loads in
+// flight per wave).
+template <int NL, int NN, bool VEC>
+__global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL, NN, VEC> a) {
+  constexpr int W = VEC ? 4 : 1;
+  constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
+
+  uint32_t xa[kStSrc][W], al[L1][W], rx[kStOut][W], ob[N1][W];
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int m = 0; m < kStSrc; ++m)
+    if (m < a.na) ld<VEC>(xa[m], row_addr(a.asrc[m], stripe, off), nb);
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int q = 0; q < L1; ++q)
+#pragma unroll
+    for (int w = 0; w < W; ++w) al[q][w] = 0u;
+  if constexpr (NL > 0) {
+#pragma unroll
+    for (int m = 0; m < kStSrc; m += 2) {
+      if (m + 1 < a.nd) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+      else if (m < a.nd) rows_mac1<NL, W>(al, a.at[m], xa[m]);
+    }
+#pragma unroll
+    for (int q = 0; q < NL; ++q)
+      if (q < a.nl) st<VEC>(al[q], row_addr(a.adst[q], stripe, off), nb);
+  }
+#pragma unroll
+  for (int r = 0; r < kStOut; ++r) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) rx[r][w] = 0u;
+    if (r < a.nr) abar_xor<NL, W>(rx[r], a.rmask[r], xa, al);
+  }
+#pragma unroll
+  for (int u = 0; u < N1; ++u) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) ob[u][w] = 0u;
+    if (u < NN && a.nmask[u]) abar_xor<NL, W>(ob[u], a.nmask[u], xa, al);
+  }
+
+  uint32_t xb[kStSrc][W];
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int m = 0; m < kStSrc; ++m)
+    if (m < a.nb) ld<VEC>(xb[m], row_addr(a.bsrc[m], stripe, off), nb);
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int m = 0; m < kStSrc; ++m)
+#pragma unroll
+    for (int r = 0; r < kStOut; ++r)
+      if (r < a.nr && a.rb[r] == m) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) xb[m][w] ^= rx[r][w];
+        st<VEC>(xb[m], row_addr(a.bsrc[m], stripe, off), nb);
+      }
+  if constexpr (NN > 0) {
+#pragma unroll
+    for (int m = 0; m < kStSrc; m += 2) {
+      if (m + 1 < a.nd) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+      else if (m < a.nd) rows_mac1<NN, W>(ob, a.bt[m], xb[m]);
+    }
+#pragma unroll
+    for (int u = 0; u < NN; ++u)
+      if (u < a.nn) st<VEC>(ob[u], row_addr(a.bdst[u], stripe, off), nb);
+  }
+}
+
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
@@ -469,6 +546,21 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     a.nmask[q] = p.nmask[q];
   }
   a.bstore = p.bstore;
+  a.nr = 0;
+  bool late = true;
+  for (int m = 0; m < kStSrc; ++m) {
+    if (!p.bret[m]) continue;
+    if (a.nr == kStOut || !((p.bstore >> m) & 1u)) {
+      late = false;
+      break;
+    }
+    a.rb[a.nr] = m;
+    a.rmask[a.nr++] = p.bret[m];
+  }
+  // Late-b is the default (measured faster: profiles/r01_bench_multi_staged.log);
+  // XRS_STAGED_LATE=0 selects the all-loads-first kernel.
+  const char* lv = std::getenv("XRS_STAGED_LATE");
+  late = late && !(lv && lv[0] == '0');
   a.nd = p.nd;
   a.na = p.na;
   a.nb = p.nb;
@@ -479,8 +571,12 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((staged_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
-                     0, stream, a);
+  if (late)
+    hipLaunchKernelGGL((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, stream, a);
+  else
+    hipLaunchKernelGGL((staged_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());
 }
 

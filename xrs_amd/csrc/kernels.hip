@@ -223,13 +223,24 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> 
 #pragma unroll
       for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
   } else {
-    for (int c = 0; c < a.n_src; ++c) {
-      uint32_t xa[W], xb[W];
-      const uint64_t s = row_addr(a.src[c], stripe, off);
-      ld<VEC>(xa, s, nb);
-      ld<VEC>(xb, s + a.half, nb);
-      pair_mac1<P, W>(acc_a, acc_b, a.tab[c], xa, xb);
-      piggyback<P, W>(acc_b, a.pbmask, c, xa);
+    // Runtime source count: groups of kGrp sources, each group's loads issued
+    // together (wave-uniform guards keep the register indexes static).
+    constexpr int kGrp = 6;
+    for (int c0 = 0; c0 < a.n_src; c0 += kGrp) {
+      uint32_t xa[kGrp][W], xb[kGrp][W];
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (c0 + g < a.n_src) {
+          const uint64_t s = row_addr(a.src[c0 + g], stripe, off);
+          ld<VEC>(xa[g], s, nb);
+          ld<VEC>(xb[g], s + a.half, nb);
+        }
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (c0 + g < a.n_src) {
+          pair_mac1<P, W>(acc_a, acc_b, a.tab[c0 + g], xa[g], xb[g]);
+          piggyback<P, W>(acc_b, a.pbmask, c0 + g, xa[g]);
+        }
     }
   }
 
@@ -333,6 +344,9 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
 #pragma unroll
     for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
   } else {
+    // Runtime counts: one row at a time (measured: grouping 8 loads per
+    // wave helped 4 KiB rows by 1-6% but cost 3-4% at 1 MiB;
+    // profiles/r01_bench_configs_grouped.log).
     for (int m = 0; m < a.nm; ++m) {
       uint32_t v[W];
       ld<VEC>(v, row_addr(a.msrc[m], stripe, off), nb);
@@ -667,7 +681,7 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
 
 template <int R, bool ACC, bool VEC>
 int launch_rows_c(const RowsPlan& p, hipStream_t s) {
-  if constexpr (R == 2 && !ACC) {
+  if constexpr (R == 2 && !ACC && VEC) {  // (the byte path of this shape would use scratch)
     if (p.NM == 12 && p.NX == 4) return launch_rows_t<2, 12, 4, ACC, VEC>(p, s);  // 12+4 ReconstOne
   }
   return launch_rows_t<R, kDyn, kDyn, ACC, VEC>(p, s);

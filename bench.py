@@ -46,19 +46,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(seconds: float, enc_bytes_step: float, rec_bytes_step: float):
-    """The oracle's CPU path (AVX2 low/high-nibble tables + separate piggyback
-    pass, i.e. the reference's algorithm) on a bounded sample, 1 thread."""
-    from oracle.oracle_c import OracleXRS, lib
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    o = OracleXRS(D, P)
+
+def _cpu_rates(o, seconds: float, threads: int):
+    """(Encode B/s, ReconstOne B/s) of the oracle's batch path on `threads`."""
     rng = np.random.Generator(np.random.PCG64(1))
     n_enc = 4096  # 256 MiB of 4 KiB stripes
     buf = rng.integers(0, 256, size=(n_enc, D + P, ENC_S), dtype=np.uint8)
-    o.encode_batch(buf, ENC_S, n_enc)  # warm
+    o.encode_batch(buf, ENC_S, n_enc, threads)  # warm
     t0, reps = time.perf_counter(), 0
     while True:
-        o.encode_batch(buf, ENC_S, n_enc)
+        o.encode_batch(buf, ENC_S, n_enc, threads)
         reps += 1
         if time.perf_counter() - t0 > seconds / 2:
             break
@@ -66,26 +73,49 @@ def cpu_baseline(seconds: float, enc_bytes_step: float, rec_bytes_step: float):
     del buf
     n_rec = 64  # 1 GiB of 1 MiB stripes
     buf = rng.integers(0, 256, size=(n_rec, D + P, REC_S), dtype=np.uint8)
-    o.encode_batch(buf, REC_S, n_rec)
+    o.encode_batch(buf, REC_S, n_rec, threads)
     t0, reps = time.perf_counter(), 0
     while True:
-        o.reconst_one_batch(buf, REC_S, n_rec, reps % D)
+        o.reconst_one_batch(buf, REC_S, n_rec, reps % D, threads)
         reps += 1
         if time.perf_counter() - t0 > seconds / 2:
             break
     rec_rate = reps * n_rec * 9 * REC_S / (time.perf_counter() - t0)
-    del buf
-    # same byte mix as one GPU step
-    t_step = enc_bytes_step / enc_rate + rec_bytes_step / rec_rate
-    value = (enc_bytes_step + rec_bytes_step) / t_step / 2**30
+    return enc_rate, rec_rate
+
+
+def cpu_baseline(seconds: float, enc_bytes_step: float, rec_bytes_step: float):
+    """The oracle's CPU path (AVX2 low/high-nibble tables + separate piggyback
+    pass, i.e. the reference's algorithm) on a bounded sample: 1 thread (the
+    reported value), then the box's CPU share (up to 16 threads)."""
+    from oracle.oracle_c import OracleXRS, lib
+
+    o = OracleXRS(D, P)
+
+    def mix(enc_rate, rec_rate):  # same byte mix as one GPU step
+        t_step = enc_bytes_step / enc_rate + rec_bytes_step / rec_rate
+        return (enc_bytes_step + rec_bytes_step) / t_step / 2**30
+
+    enc1, rec1 = _cpu_rates(o, seconds, 1)
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    threads = max(1, min(16, share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    encn, recn = _cpu_rates(o, seconds / 2, threads)
     return {
-        "value": round(value, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "value": round(mix(enc1, rec1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
         "simd": "avx2" if lib().oxrs_simd_available() else "scalar",
-        "encode_gibps": round(enc_rate / 2**30, 3),
-        "reconst_one_gibps": round(rec_rate / 2**30, 3),
-        "sample": (f"oracle/xrs_oracle.c, 1 thread: Encode of {n_enc} 12+4 stripes @ 4 KiB "
-                   f"(256 MiB) and ReconstOne of {n_rec} stripes @ 1 MiB (1 GiB), each repeated "
-                   f"for {seconds / 2:.0f} s; combined with the GPU step's byte mix"),
+        "cpu_model": _cpu_model(),
+        "encode_gibps": round(enc1 / 2**30, 3),
+        "reconst_one_gibps": round(rec1 / 2**30, 3),
+        "multi_thread": {"threads": threads, "value": round(mix(encn, recn), 3),
+                         "encode_gibps": round(encn / 2**30, 3),
+                         "reconst_one_gibps": round(recn / 2**30, 3)},
+        "sample": (f"oracle/xrs_oracle.c: Encode of 4096 12+4 stripes @ 4 KiB (256 MiB) and "
+                   f"ReconstOne of 64 stripes @ 1 MiB (1 GiB), repeated for {seconds / 2:.0f} s "
+                   f"each on 1 thread and {seconds / 4:.0f} s each on {threads} threads; "
+                   f"combined with the GPU step's byte mix"),
     }
 
 

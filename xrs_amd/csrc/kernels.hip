@@ -216,12 +216,17 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> 
     for (int c = 0; c + 1 < C; c += 2)
       pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
     if constexpr (C & 1) pair_mac1<P, W>(acc_a, acc_b, a.tab[C - 1], xa[C - 1], xb[C - 1]);
-    // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
-    // c rides on parity 1 + c % (P-1).  Only used for full-width Encode.
+    if constexpr (C == 12 && !ACC) {
+      // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
+      // c rides on parity 1 + c % (P-1).  Only used for full-width Encode.
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+      for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+        for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) piggyback<P, W>(acc_b, a.pbmask, c, xa[c]);
+    }
   } else {
     // Runtime source count: groups of kGrp sources, each group's loads issued
     // together (wave-uniform guards keep the register indexes static).
@@ -471,6 +476,7 @@ __global__ __launch_bounds__(kBlock) void staged_kernel(const StagedArgs<NL, NN,
 // flight per wave).
 template <int NL, int NN, bool VEC>
 __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL, NN, VEC> a) {
+  const int nd = a.nd;
   constexpr int W = VEC ? 4 : 1;
   constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -492,8 +498,8 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   if constexpr (NL > 0) {
 #pragma unroll
     for (int m = 0; m < kStSrc; m += 2) {
-      if (m + 1 < a.nd) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
-      else if (m < a.nd) rows_mac1<NL, W>(al, a.at[m], xa[m]);
+      if (m + 1 < nd) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+      else if (m < nd) rows_mac1<NL, W>(al, a.at[m], xa[m]);
     }
 #pragma unroll
     for (int q = 0; q < NL; ++q)
@@ -530,8 +536,8 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   if constexpr (NN > 0) {
 #pragma unroll
     for (int m = 0; m < kStSrc; m += 2) {
-      if (m + 1 < a.nd) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
-      else if (m < a.nd) rows_mac1<NN, W>(ob, a.bt[m], xb[m]);
+      if (m + 1 < nd) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+      else if (m < nd) rows_mac1<NN, W>(ob, a.bt[m], xb[m]);
     }
 #pragma unroll
     for (int u = 0; u < NN; ++u)
@@ -585,6 +591,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  // (A compile-time survivor count, ND = 12, let the scheduler hoist the
+  // b-row loads: 225-232 VGPRs plus scratch.  Runtime nd only.)
   if (late)
     hipLaunchKernelGGL((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, stream, a);
@@ -641,6 +649,8 @@ int launch_pair_c(const PairPlan& p, hipStream_t s) {
   if constexpr (P == 4 && !ACC) {
     if (p.C == 12 && p.encode12) return launch_pair_t<4, 12, ACC, VEC>(p, s);  // 12+4 Encode
   }
+  // (Compile-time Update (C=2) and Replace(4) shapes measured no faster than
+  // the runtime kernel at 8 MiB: profiles/r01_bench_configs_c4_ct.log.)
   return launch_pair_t<P, kDyn, ACC, VEC>(p, s);
 }
 

@@ -2,15 +2,19 @@
 """Headline benchmark of the MI355X X-Reed-Solomon codec.
 
 Metric (BASELINE.json): "Encode + 1-lost Reconstruct GiB/s (device-resident),
-12+4 @ 4KiB/1MiB".  One step = one pass of the hot path over one batch:
+12+4 @ 4KiB/1MiB".  One step = one pass of the hot path over one batch of each
+of the four (operation, vect size) pairs the north star names:
 
   * Encode (xrs.go:103) of `--enc-stripes` 12+4 stripes of 4 KiB vects
     (65,536 stripes = 4 GiB; algorithmic bytes (d+p)*S per stripe, the
-    reference's SetBytes, xrs_test.go:513), then
-  * ReconstOne (xrs.go:175, via Reconst with one lost data vect) of
-    `--rec-stripes` 12+4 stripes of 1 MiB vects (512 stripes = 8 GiB buffer;
-    bytes 9*S per stripe = 8*S read + S written, xrs_test.go:565-572).
+    reference's SetBytes, xrs_test.go:513);
+  * ReconstOne (xrs.go:175, Reconst with one lost data vect) of the same
+    4 KiB stripes (bytes 9*S per stripe = 8*S read + S written,
+    xrs_test.go:565-572);
+  * Encode of `--rec-stripes` 12+4 stripes of 1 MiB vects (512 stripes = 8 GiB);
+  * ReconstOne of the same 1 MiB stripes.
 
+ReconstOne rebuilds data shard k = step mod 12.
 value = algorithmic bytes of all ranks / max-over-ranks time, in GiB/s.  Inputs
 are synthetic, generated on the device, and resident in HBM before timing.
 Multi-GPU: one process per GPU, each with its own batch (weak scaling, no
@@ -58,33 +62,32 @@ def _cpu_model() -> str:
 
 
 def _cpu_rates(o, seconds: float, threads: int):
-    """(Encode B/s, ReconstOne B/s) of the oracle's batch path on `threads`."""
+    """Bytes/s of the oracle's batch path on `threads` for the four bench
+    kernels, each run for seconds/4 on a bounded sample."""
     rng = np.random.Generator(np.random.PCG64(1))
-    n_enc = 4096  # 256 MiB of 4 KiB stripes
-    buf = rng.integers(0, 256, size=(n_enc, D + P, ENC_S), dtype=np.uint8)
-    o.encode_batch(buf, ENC_S, n_enc, threads)  # warm
-    t0, reps = time.perf_counter(), 0
-    while True:
-        o.encode_batch(buf, ENC_S, n_enc, threads)
-        reps += 1
-        if time.perf_counter() - t0 > seconds / 2:
-            break
-    enc_rate = reps * n_enc * (D + P) * ENC_S / (time.perf_counter() - t0)
-    del buf
-    n_rec = 64  # 1 GiB of 1 MiB stripes
-    buf = rng.integers(0, 256, size=(n_rec, D + P, REC_S), dtype=np.uint8)
-    o.encode_batch(buf, REC_S, n_rec, threads)
-    t0, reps = time.perf_counter(), 0
-    while True:
-        o.reconst_one_batch(buf, REC_S, n_rec, reps % D, threads)
-        reps += 1
-        if time.perf_counter() - t0 > seconds / 2:
-            break
-    rec_rate = reps * n_rec * 9 * REC_S / (time.perf_counter() - t0)
-    return enc_rate, rec_rate
+
+    def run(fn, nbytes):
+        fn(0)  # warm
+        t0, reps = time.perf_counter(), 0
+        while True:
+            fn(reps)
+            reps += 1
+            if time.perf_counter() - t0 > seconds / 4:
+                break
+        return reps * nbytes / (time.perf_counter() - t0)
+
+    rates = {}
+    for key, size, n in (("4k", ENC_S, 16384), ("1m", REC_S, 64)):  # 1 GiB each (> LLC)
+        buf = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+        rates["encode_" + key] = run(lambda i: o.encode_batch(buf, size, n, threads),
+                                     n * (D + P) * size)
+        rates["reconst_one_" + key] = run(
+            lambda i: o.reconst_one_batch(buf, size, n, i % D, threads), n * 9 * size)
+        del buf
+    return rates
 
 
-def cpu_baseline(seconds: float, enc_bytes_step: float, rec_bytes_step: float):
+def cpu_baseline(seconds: float, step_bytes: dict):
     """The oracle's CPU path (AVX2 low/high-nibble tables + separate piggyback
     pass, i.e. the reference's algorithm) on a bounded sample: 1 thread (the
     reported value), then the box's CPU share (up to 16 threads)."""
@@ -92,30 +95,28 @@ def cpu_baseline(seconds: float, enc_bytes_step: float, rec_bytes_step: float):
 
     o = OracleXRS(D, P)
 
-    def mix(enc_rate, rec_rate):  # same byte mix as one GPU step
-        t_step = enc_bytes_step / enc_rate + rec_bytes_step / rec_rate
-        return (enc_bytes_step + rec_bytes_step) / t_step / 2**30
+    def mix(rates):  # same byte mix as one GPU step
+        t_step = sum(step_bytes[k] / rates[k] for k in step_bytes)
+        return sum(step_bytes.values()) / t_step / 2**30
 
-    enc1, rec1 = _cpu_rates(o, seconds, 1)
+    r1 = _cpu_rates(o, seconds, 1)
     try:
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count() or 1
     threads = max(1, min(16, share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    encn, recn = _cpu_rates(o, seconds / 2, threads)
+    rn = _cpu_rates(o, seconds / 2, threads)
     return {
-        "value": round(mix(enc1, rec1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "value": round(mix(r1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
         "simd": "avx2" if lib().oxrs_simd_available() else "scalar",
         "cpu_model": _cpu_model(),
-        "encode_gibps": round(enc1 / 2**30, 3),
-        "reconst_one_gibps": round(rec1 / 2**30, 3),
-        "multi_thread": {"threads": threads, "value": round(mix(encn, recn), 3),
-                         "encode_gibps": round(encn / 2**30, 3),
-                         "reconst_one_gibps": round(recn / 2**30, 3)},
-        "sample": (f"oracle/xrs_oracle.c: Encode of 4096 12+4 stripes @ 4 KiB (256 MiB) and "
-                   f"ReconstOne of 64 stripes @ 1 MiB (1 GiB), repeated for {seconds / 2:.0f} s "
-                   f"each on 1 thread and {seconds / 4:.0f} s each on {threads} threads; "
-                   f"combined with the GPU step's byte mix"),
+        "gibps": {k: round(v / 2**30, 3) for k, v in r1.items()},
+        "multi_thread": {"threads": threads, "value": round(mix(rn), 3),
+                         "gibps": {k: round(v / 2**30, 3) for k, v in rn.items()}},
+        "sample": (f"oracle/xrs_oracle.c: Encode and ReconstOne of 16384 12+4 stripes @ 4 KiB "
+                   f"(1 GiB) and of 64 stripes @ 1 MiB (1 GiB), each repeated for "
+                   f"{seconds / 4:.1f} s on 1 thread and {seconds / 8:.1f} s on {threads} "
+                   f"threads; combined with the GPU step's byte mix"),
     }
 
 
@@ -137,7 +138,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--enc-stripes", type=int, default=65536)
     ap.add_argument("--rec-stripes", type=int, default=512)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -173,25 +174,39 @@ def main():
                             generator=g)
     rec_buf = torch.randint(0, 256, (n_rec * rec_stripe,), dtype=torch.uint8, device=dev,
                             generator=g)
+    x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
     x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, stream)
     torch.cuda.synchronize()
-    enc_bytes = n_enc * (D + P) * ENC_S          # per launch, algorithmic (read + write)
-    rec_bytes = n_rec * 9 * REC_S
-
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # The four timed launches of a step, in order: (key, kernel, algorithmic
+    # bytes per launch, read bytes per launch, launcher).
+    launches = [
+        ("encode_4k", "pair_kernel<4,12,false,true>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
+         lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
+                                    stream)),
+        ("reconst_one_4k", "rows_kernel<2,12,4,false,true>", n_enc * 9 * ENC_S,
+         n_enc * 8 * ENC_S,
+         lambda i: x.reconst_one_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
+                                         i % D, stream)),
+        ("encode_1m", "pair_kernel<4,12,false,true>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
+         lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
+                                    stream)),
+        ("reconst_one_1m", "rows_kernel<2,12,4,false,true>", n_rec * 9 * REC_S,
+         n_rec * 8 * REC_S,
+         lambda i: x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
+                                         i % D, stream)),
+    ]
+    launches = [l for l in launches if l[2] > 0]
+    step_bytes = sum(l[2] for l in launches)
+    nl = len(launches)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(nl + 1)] for _ in range(args.steps)]
 
     def step(i, events=None):
+        for j, l in enumerate(launches):
+            if events:
+                events[j].record()
+            l[4](i)
         if events:
-            events[0].record()
-        if n_enc:
-            x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
-        if events:
-            events[1].record()
-        if n_rec:
-            x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
-                                  i % D, stream)
-        if events:
-            events[2].record()
+            events[nl].record()
 
     for i in range(args.warmup):
         step(i)
@@ -208,34 +223,25 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
-
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    total_bytes = world * args.steps * (enc_bytes + rec_bytes)
+    total_bytes = world * args.steps * step_bytes
     value = total_bytes / elapsed_max / 2**30
 
     kernels = {}
-    if n_enc:
-        kernels["encode_4k"] = {
-            "kernel": "pair_kernel<4,12,false,true>", "ms": round(enc_ms, 4),
-            "bytes_per_launch": enc_bytes,
-            "gibps": round(enc_bytes / (enc_ms / 1e3) / 2**30, 1),
-            "achieved_gbs": round(enc_bytes / (enc_ms / 1e3) / 1e9, 1),
-            "read_only_gbs": round(n_enc * D * ENC_S / (enc_ms / 1e3) / 1e9, 1),
-        }
-    if n_rec:
-        kernels["reconst_one_1m"] = {
-            "kernel": "rows_kernel<2,12,4,false,true>", "ms": round(rec_ms, 4),
-            "bytes_per_launch": rec_bytes,
-            "gibps": round(rec_bytes / (rec_ms / 1e3) / 2**30, 1),
-            "achieved_gbs": round(rec_bytes / (rec_ms / 1e3) / 1e9, 1),
-            "read_only_gbs": round(n_rec * 8 * REC_S / (rec_ms / 1e3) / 1e9, 1),
+    for j, (key, kname, nbytes, rbytes, _) in enumerate(launches):
+        ms = float(np.mean([e[j].elapsed_time(e[j + 1]) for e in ev]))
+        kernels[key] = {
+            "kernel": kname, "ms": round(ms, 4), "bytes_per_launch": nbytes,
+            "gibps": round(nbytes / (ms / 1e3) / 2**30, 1),
+            "achieved_gbs": round(nbytes / (ms / 1e3) / 1e9, 1),
+            "frac": round(nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "read_only_gbs": round(rbytes / (ms / 1e3) / 1e9, 1),
         }
     dom_key = max(kernels, key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_key]
     traffic = pmc_traffic(dom_key)
     roofline = {
-        "bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved_gbs"],
+        "bound": "hbm", "kernel": dom["kernel"], "launch": dom_key,
+        "achieved": dom["achieved_gbs"],
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom["achieved_gbs"] / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
@@ -244,7 +250,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing CPU baseline ...")
-        cpu = cpu_baseline(args.cpu_seconds, enc_bytes, rec_bytes)
+        cpu = cpu_baseline(args.cpu_seconds, {l[0]: l[2] for l in launches})
 
     if rank == 0:
         out = {
@@ -261,8 +267,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform random bytes generated on device, seeded per rank)",
             "config": {
-                "workload": (f"12+4 Encode of {n_enc} stripes @ 4 KiB + ReconstOne (k = step mod 12)"
-                             f" of {n_rec} stripes @ 1 MiB per GPU per step"),
+                "workload": (f"12+4 Encode + ReconstOne (k = step mod 12) of {n_enc} stripes "
+                             f"@ 4 KiB and of {n_rec} stripes @ 1 MiB, per GPU per step"),
                 "data_shards": D, "parity_shards": P,
                 "encode_vect_bytes": ENC_S, "encode_stripes_per_gpu": n_enc,
                 "reconst_vect_bytes": REC_S, "reconst_stripes_per_gpu": n_rec,

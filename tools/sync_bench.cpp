@@ -28,16 +28,31 @@ int main(int argc, char** argv) {
     std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, 1));
     std::vector<uint8_t*> p;
     for (auto& x : v) p.push_back(x.data());
-    xrs_encode(c, p.data(), 16, size);
-    long n = 0;
-    const double t0 = now();
-    while (now() - t0 < seconds) {
-      if (xrs_encode(c, p.data(), 16, size)) return 3;
-      ++n;
-    }
-    const double dt = (now() - t0) / n;
-    std::printf("{\"api\": \"xrs_encode\", \"vect_bytes\": %zu, \"threads\": 1, \"us_per_call\": %.1f, "
-                "\"gibps\": %.3f}\n", size, dt * 1e6, 16.0 * size / dt / (1 << 30));
+    auto timeit = [&](const char* api, double bytes, auto&& call) {
+      if (call()) std::exit(3);
+      long n = 0;
+      const double t0 = now();
+      while (now() - t0 < seconds) {
+        if (call()) std::exit(3);
+        ++n;
+      }
+      const double dt = (now() - t0) / n;
+      std::printf("{\"api\": \"%s\", \"vect_bytes\": %zu, \"threads\": 1, \"us_per_call\": %.1f, "
+                  "\"gibps\": %.3f}\n", api, size, dt * 1e6, bytes / dt / (1 << 30));
+      std::fflush(stdout);
+    };
+    timeit("xrs_encode", 16.0 * size, [&] { return xrs_encode(c, p.data(), 16, size); });
+    timeit("xrs_reconst_one", 9.0 * size, [&] { return xrs_reconst_one(c, p.data(), 16, size, 0); });
+    const int has[] = {2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, need[] = {0, 1};
+    timeit("xrs_reconst_2", 14.0 * size,
+           [&] { return xrs_reconst(c, p.data(), 16, size, has, 14, need, 2); });
+    timeit("xrs_update", 10.0 * size,
+           [&] { return xrs_update(c, p[0], p[1], size, 0, p.data() + 12, 4); });
+  }
+  if (argc > 2 && std::strcmp(argv[2], "sync") == 0) {
+    xrs_free(c);
+    std::fflush(stdout);
+    std::_Exit(0);
   }
   // --- batching queue, T threads
   for (int threads : {1, 8, 32, 128}) {

@@ -39,7 +39,8 @@ struct xrs_codec {
   mutable std::mutex mu;
   mutable uint8_t* staging = nullptr;
   mutable size_t staging_cap = 0;
-  mutable uint8_t* hstaging = nullptr;  // pinned host mirror of `staging` (small stripes)
+  mutable uint8_t* hstaging = nullptr;  // pinned, mapped host mirror of `staging` (small calls)
+  mutable uint8_t* hstaging_dev = nullptr;  // its device address (zero-copy kernels)
   mutable size_t hstaging_cap = 0;
   mutable hipStream_t stream = nullptr;
 
@@ -545,33 +546,113 @@ int ensure_staging(const xrs_codec* x, size_t bytes) {
   return XRS_OK;
 }
 
-// Small stripes go through a pinned host mirror of the device staging: the
-// caller's vects are gathered by CPU memcpy, then ONE H2D, the kernel and ONE
-// D2H (instead of one small copy per vect, each a few microseconds).
-constexpr size_t kPinnedStageMax = 8u << 20;
-
 int ensure_hstaging(const xrs_codec* x, size_t bytes) {
   if (bytes > x->hstaging_cap) {
     if (x->hstaging) (void)hipHostFree(x->hstaging);
-    x->hstaging = nullptr;
+    x->hstaging = x->hstaging_dev = nullptr;
     x->hstaging_cap = 0;
     const size_t cap = std::max<size_t>(bytes, 1 << 20);
-    if (hipHostMalloc(&x->hstaging, cap, hipHostMallocDefault) != hipSuccess) return XRS_ERR_HIP;
+    if (hipHostMalloc(&x->hstaging, cap, hipHostMallocMapped) != hipSuccess) return XRS_ERR_HIP;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, x->hstaging, 0) == hipSuccess) x->hstaging_dev = static_cast<uint8_t*>(dp);
     x->hstaging_cap = cap;
   }
   return XRS_OK;
 }
 
-int h2d(const xrs_codec* x, size_t off, const void* src, size_t n) {
-  if (n == 0) return XRS_OK;
-  if (!src) return XRS_ERR_INVALID_ARG;
-  return hip_err(hipMemcpyAsync(x->staging + off, src, n, hipMemcpyHostToDevice, x->stream));
-}
-int d2h(const xrs_codec* x, void* dst, size_t off, size_t n) {
-  if (n == 0) return XRS_OK;
-  return hip_err(hipMemcpyAsync(dst, x->staging + off, n, hipMemcpyDeviceToHost, x->stream));
-}
 int sync(const xrs_codec* x) { return hip_err(hipStreamSynchronize(x->stream)); }
+
+size_t env_size(const char* name, size_t dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? static_cast<size_t>(std::strtoull(v, nullptr, 0)) : dflt;
+}
+
+// The transfers of one synchronous call (xrs_encode ... xrs_replace), laid out
+// as `total` bytes of staging rows:
+//  * ZeroCopy (total <= XRS_SYNC_ZC_MAX, default 256 KiB): inputs are
+//    gathered by CPU memcpy into the pinned mirror and the kernel reads and
+//    writes the mirror in place over PCIe: no DMA, one launch, one sync.
+//  * Pinned (total <= 8 MiB): the same gather, then one H2D of the touched
+//    span, the kernel, one D2H of the written span.
+//  * Direct: one copy per vect straight to / from device staging.
+// Outputs are scattered to the caller's buffers after the sync.
+class Stage {
+ public:
+  enum Mode { kZeroCopy, kPinned, kDirect };
+
+  Stage(const xrs_codec* x, size_t total) : x_(x), total_(std::max<size_t>(total, 1)) {}
+
+  int init() {
+    int e = ensure_staging(x_, mode_for() == kZeroCopy ? 1 : total_);  // also creates the stream
+    if (e) return e;
+    mode_ = mode_for();
+    if (mode_ != kDirect) {
+      if ((e = ensure_hstaging(x_, total_))) return e;
+      if (mode_ == kZeroCopy && !x_->hstaging_dev) {
+        mode_ = kPinned;
+        if ((e = ensure_staging(x_, total_))) return e;
+      }
+    }
+    return XRS_OK;
+  }
+  uint8_t* base() const { return mode_ == kZeroCopy ? x_->hstaging_dev : x_->staging; }
+  Layout layout(size_t shard_stride, size_t off = 0) const { return {base() + off, shard_stride, total_}; }
+
+  int in(size_t off, const void* src, size_t n) {
+    if (n == 0) return XRS_OK;
+    if (!src) return XRS_ERR_INVALID_ARG;
+    if (mode_ == kDirect)
+      return hip_err(hipMemcpyAsync(x_->staging + off, src, n, hipMemcpyHostToDevice, x_->stream));
+    std::memcpy(x_->hstaging + off, src, n);
+    in_lo_ = std::min(in_lo_, off);
+    in_hi_ = std::max(in_hi_, off + n);
+    return XRS_OK;
+  }
+  // After the last in(), before the kernel.
+  int upload() {
+    if (mode_ != kPinned || in_hi_ <= in_lo_) return XRS_OK;
+    return hip_err(hipMemcpyAsync(x_->staging + in_lo_, x_->hstaging + in_lo_, in_hi_ - in_lo_,
+                                  hipMemcpyHostToDevice, x_->stream));
+  }
+  void out(void* dst, size_t off, size_t n) {
+    if (n == 0) return;
+    outs_.push_back({dst, off, n});
+    out_lo_ = std::min(out_lo_, off);
+    out_hi_ = std::max(out_hi_, off + n);
+  }
+  // After the kernel(s): download, sync, scatter.  Returns a transfer error.
+  int finish() {
+    int e = XRS_OK;
+    if (mode_ == kDirect) {
+      for (const Out& o : outs_)
+        if (!e) e = hip_err(hipMemcpyAsync(o.dst, x_->staging + o.off, o.n, hipMemcpyDeviceToHost, x_->stream));
+    } else if (mode_ == kPinned && out_hi_ > out_lo_) {
+      e = hip_err(hipMemcpyAsync(x_->hstaging + out_lo_, x_->staging + out_lo_, out_hi_ - out_lo_,
+                                 hipMemcpyDeviceToHost, x_->stream));
+    }
+    const int es = sync(x_);
+    if (e || es) return e ? e : es;
+    if (mode_ != kDirect)
+      for (const Out& o : outs_) std::memcpy(o.dst, x_->hstaging + o.off, o.n);
+    return XRS_OK;
+  }
+
+ private:
+  struct Out {
+    void* dst;
+    size_t off, n;
+  };
+  Mode mode_for() const {
+    if (total_ <= env_size("XRS_SYNC_ZC_MAX", 256u << 10)) return kZeroCopy;
+    if (total_ <= env_size("XRS_SYNC_PINNED_MAX", 8u << 20)) return kPinned;
+    return kDirect;
+  }
+  const xrs_codec* x_;
+  size_t total_;
+  Mode mode_ = kDirect;
+  size_t in_lo_ = SIZE_MAX, in_hi_ = 0, out_lo_ = SIZE_MAX, out_hi_ = 0;
+  std::vector<Out> outs_;
+};
 
 // ---------------------------------------------------- host-resident pipeline
 constexpr size_t kChunkBytes = 64u << 20;  // device bytes per pipeline chunk
@@ -1047,28 +1128,15 @@ int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
   if (size == 0) return XRS_OK;
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  const size_t total = static_cast<size_t>(n) * size, dbytes = static_cast<size_t>(x->d) * size;
-  if ((e = ensure_staging(x, total))) return e;
-  const Layout L{x->staging, size, total};
-  if (total <= kPinnedStageMax) {
-    if ((e = ensure_hstaging(x, total))) return e;
-    for (int j = 0; j < x->d; ++j) std::memcpy(x->hstaging + static_cast<size_t>(j) * size, vects[j], size);
-    e = hip_err(hipMemcpyAsync(x->staging, x->hstaging, dbytes, hipMemcpyHostToDevice, x->stream));
-    if (!e) e = encode_impl(x, L, size, 1, x->stream);
-    if (!e)
-      e = hip_err(hipMemcpyAsync(x->hstaging + dbytes, x->staging + dbytes, total - dbytes,
-                                 hipMemcpyDeviceToHost, x->stream));
-    const int es = sync(x);
-    if (e || es) return e ? e : es;
+  Stage st(x, static_cast<size_t>(n) * size);
+  if ((e = st.init())) return e;
+  for (int j = 0; j < x->d && !e; ++j) e = st.in(static_cast<size_t>(j) * size, vects[j], size);
+  if (!e) e = st.upload();
+  if (!e) e = encode_impl(x, st.layout(size), size, 1, x->stream);
+  if (!e)
     for (int r = 0; r < x->p; ++r)
-      std::memcpy(vects[x->d + r], x->hstaging + dbytes + static_cast<size_t>(r) * size, size);
-    return XRS_OK;
-  }
-  for (int j = 0; j < x->d && !e; ++j) e = h2d(x, static_cast<size_t>(j) * size, vects[j], size);
-  if (!e) e = encode_impl(x, L, size, 1, x->stream);
-  for (int r = 0; r < x->p && !e; ++r)
-    e = d2h(x, vects[x->d + r], static_cast<size_t>(x->d + r) * size, size);
-  const int es = sync(x);
+      st.out(vects[x->d + r], static_cast<size_t>(x->d + r) * size, size);
+  const int es = st.finish();
   return e ? e : es;
 }
 
@@ -1094,34 +1162,16 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
   if (!vects[k]) return XRS_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  const size_t total = static_cast<size_t>(n) * size;
-  if ((e = ensure_staging(x, total))) return e;
-  const Layout L{x->staging, size, total};
-  if (total <= kPinnedStageMax) {
-    // Gather the need-set halves into the pinned mirror at their device
-    // offsets; bytes the kernel does not read travel as don't-care.
-    if ((e = ensure_hstaging(x, total))) return e;
-    for (auto& r : reads)
-      std::memcpy(x->hstaging + static_cast<size_t>(r.first) * size + r.second * half,
-                  vects[r.first] + r.second * half, half);
-    e = hip_err(hipMemcpyAsync(x->staging, x->hstaging, total, hipMemcpyHostToDevice, x->stream));
-    if (!e) e = reconst_one_impl(x, L, size, 1, k, x->stream);
-    const size_t ko = static_cast<size_t>(k) * size;
-    if (!e)
-      e = hip_err(hipMemcpyAsync(x->hstaging + ko, x->staging + ko, size, hipMemcpyDeviceToHost,
-                                 x->stream));
-    const int es = sync(x);
-    if (e || es) return e ? e : es;
-    std::memcpy(vects[k], x->hstaging + ko, size);
-    return XRS_OK;
-  }
+  Stage st(x, static_cast<size_t>(n) * size);
+  if ((e = st.init())) return e;
   for (size_t i = 0; i < reads.size() && !e; ++i) {
     const size_t off = static_cast<size_t>(reads[i].first) * size + reads[i].second * half;
-    e = h2d(x, off, vects[reads[i].first] + reads[i].second * half, half);
+    e = st.in(off, vects[reads[i].first] + reads[i].second * half, half);
   }
-  if (!e) e = reconst_one_impl(x, L, size, 1, k, x->stream);
-  if (!e) e = d2h(x, vects[k], static_cast<size_t>(k) * size, size);
-  const int es = sync(x);
+  if (!e) e = st.upload();
+  if (!e) e = reconst_one_impl(x, st.layout(size), size, 1, k, x->stream);
+  if (!e) st.out(vects[k], static_cast<size_t>(k) * size, size);
+  const int es = st.finish();
   return e ? e : es;
 }
 
@@ -1137,25 +1187,25 @@ int xrs_reconst(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, c
   if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(x->mu);
   DeviceGuard g(x->device);
-  if ((e = ensure_staging(x, std::max<size_t>(1, static_cast<size_t>(n) * size)))) return e;
-  for (int i = 0; i < n && !e; ++i) e = h2d(x, static_cast<size_t>(i) * size, vects[i], size);
+  Stage st(x, static_cast<size_t>(n) * size);
+  if ((e = st.init())) return e;
+  for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(i) * size, vects[i], size);
+  if (!e) e = st.upload();
   if (e) {
     (void)sync(x);
     return e;
   }
   Written w;
-  const int er = reconst_impl(x, {x->staging, size, static_cast<size_t>(n) * size}, size,
-                              size ? 1 : 0, dp_has, n_has, need, n_need, x->stream, &w);
+  const int er = reconst_impl(x, st.layout(size), size, size ? 1 : 0, dp_has, n_has, need, n_need,
+                              x->stream, &w);
   // Copy back every half the device wrote, also when a later step failed
   // (the reference's Reconst is not atomic either).
   const size_t half = size / 2;
-  for (auto& h : w.halves) {
-    if (e) break;
-    e = d2h(x, vects[h.first] + h.second * half,
-            static_cast<size_t>(h.first) * size + h.second * half, half);
-  }
-  const int es = sync(x);
-  return er ? er : (e ? e : es);
+  for (auto& h : w.halves)
+    st.out(vects[h.first] + h.second * half, static_cast<size_t>(h.first) * size + h.second * half,
+           half);
+  e = st.finish();
+  return er ? er : e;
 }
 
 // xrs.go:324-346
@@ -1173,14 +1223,17 @@ int xrs_update(const xrs_codec* x, const uint8_t* old_data, const uint8_t* new_d
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, p old, p+1 new
   const size_t stride = static_cast<size_t>(p + 2) * size;
-  if ((e = ensure_staging(x, stride))) return e;
-  for (int r = 0; r < p && !e; ++r) e = h2d(x, static_cast<size_t>(r) * size, parity[r], size);
-  if (!e) e = h2d(x, static_cast<size_t>(p) * size, old_data, size);
-  if (!e) e = h2d(x, static_cast<size_t>(p + 1) * size, new_data, size);
-  const Layout P{x->staging, size, stride};
+  Stage st(x, stride);
+  if ((e = st.init())) return e;
+  for (int r = 0; r < p && !e; ++r) e = st.in(static_cast<size_t>(r) * size, parity[r], size);
+  if (!e) e = st.in(static_cast<size_t>(p) * size, old_data, size);
+  if (!e) e = st.in(static_cast<size_t>(p + 1) * size, new_data, size);
+  if (!e) e = st.upload();
+  const Layout P = st.layout(size);
   if (!e) e = update_impl(x, P.row(p, 0), P.row(p + 1, 0), size, row, P, 1, x->stream);
-  for (int r = 0; r < p && !e; ++r) e = d2h(x, parity[r], static_cast<size_t>(r) * size, size);
-  const int es = sync(x);
+  if (!e)
+    for (int r = 0; r < p; ++r) st.out(parity[r], static_cast<size_t>(r) * size, size);
+  const int es = st.finish();
   return e ? e : es;
 }
 
@@ -1198,14 +1251,17 @@ int xrs_replace(const xrs_codec* x, uint8_t* const* data, const int* rows, int n
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, [p, p+n) data
   const size_t stride = static_cast<size_t>(p + n) * size;
-  if ((e = ensure_staging(x, stride))) return e;
-  for (int r = 0; r < p && !e; ++r) e = h2d(x, static_cast<size_t>(r) * size, parity[r], size);
-  for (int i = 0; i < n && !e; ++i) e = h2d(x, static_cast<size_t>(p + i) * size, data[i], size);
-  const Layout P{x->staging, size, stride};
-  const Layout D{x->staging + static_cast<size_t>(p) * size, size, stride};
+  Stage st(x, stride);
+  if ((e = st.init())) return e;
+  for (int r = 0; r < p && !e; ++r) e = st.in(static_cast<size_t>(r) * size, parity[r], size);
+  for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(p + i) * size, data[i], size);
+  if (!e) e = st.upload();
+  const Layout P = st.layout(size);
+  const Layout D = st.layout(size, static_cast<size_t>(p) * size);
   if (!e) e = replace_impl(x, D, rows, n, size, P, 1, x->stream);
-  for (int r = 0; r < p && !e; ++r) e = d2h(x, parity[r], static_cast<size_t>(r) * size, size);
-  const int es = sync(x);
+  if (!e)
+    for (int r = 0; r < p; ++r) st.out(parity[r], static_cast<size_t>(r) * size, size);
+  const int es = st.finish();
   return e ? e : es;
 }
 

@@ -163,10 +163,10 @@ class XRS:
         self.data_num = _lib.xrs_data_num(h)
         self.parity_num = _lib.xrs_parity_num(h)
 
-    def __del__(self):
+    def __del__(self, _free=_lib.xrs_free):  # bound now: module globals are gone at exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            _lib.xrs_free(h)
+            _free(h)
             self._h = None
 
     @property
@@ -324,9 +324,9 @@ class XRSQueue:
         self.size = size
         self.batch_stripes = _lib.xrs_queue_batch_stripes(h)
 
-    def close(self):
+    def close(self, _free=_lib.xrs_queue_free):
         if self._h is not None and self._h.value:
-            _lib.xrs_queue_free(self._h)
+            _free(self._h)
             self._h = None
 
     def __del__(self):

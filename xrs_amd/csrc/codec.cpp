@@ -569,7 +569,7 @@ size_t env_size(const char* name, size_t dflt) {
 
 // The transfers of one synchronous call (xrs_encode ... xrs_replace), laid out
 // as `total` bytes of staging rows:
-//  * ZeroCopy (total <= XRS_SYNC_ZC_MAX, default 256 KiB): inputs are
+//  * ZeroCopy (total <= XRS_SYNC_ZC_MAX, default 4 MiB): inputs are
 //    gathered by CPU memcpy into the pinned mirror and the kernel reads and
 //    writes the mirror in place over PCIe: no DMA, one launch, one sync.
 //  * Pinned (total <= 8 MiB): the same gather, then one H2D of the touched
@@ -643,7 +643,7 @@ class Stage {
     size_t off, n;
   };
   Mode mode_for() const {
-    if (total_ <= env_size("XRS_SYNC_ZC_MAX", 256u << 10)) return kZeroCopy;
+    if (total_ <= env_size("XRS_SYNC_ZC_MAX", 4u << 20)) return kZeroCopy;
     if (total_ <= env_size("XRS_SYNC_PINNED_MAX", 8u << 20)) return kPinned;
     return kDirect;
   }

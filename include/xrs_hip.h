@@ -150,10 +150,15 @@ int xrs_encode_host(const xrs_codec *codec, uint8_t *host_base, size_t size, siz
 /* ReconstOne(k) per stripe; only the GetNeedVects halves cross PCIe. */
 int xrs_reconst_one_host(const xrs_codec *codec, uint8_t *host_base, size_t size,
                          size_t shard_stride, size_t stripe_stride, size_t n_stripes, int k);
-void *xrs_host_alloc(size_t bytes);           /* pinned host memory (NULL on failure) */
+void *xrs_host_alloc(size_t bytes);           /* pinned, device-mapped host memory (NULL on failure) */
 void xrs_host_free(void *p);
-int xrs_host_register(void *p, size_t bytes); /* pin existing host memory */
+int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */
 int xrs_host_unregister(void *p);
+/* Device address of pinned, mapped host memory (from xrs_host_alloc or
+ * xrs_host_register), or NULL.  It may be passed as the base of the
+ * *_batched calls: the kernels then read and write host memory over PCIe
+ * (zero copy). */
+void *xrs_host_device_pointer(void *host);
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling

@@ -52,11 +52,54 @@ def run(op, size, n, pinned, reps):
             "h2d_gbs": round(h2d / dt / 1e9, 2), "d2h_gbs": round(d2h / dt / 1e9, 2)}
 
 
+def run_zero_copy(op, size, n, reps):
+    """The *_batched kernels run directly on pinned, mapped host memory (no
+    DMA): reads and writes cross PCIe from the kernel.  Parity is checked
+    against the oracle on the first stripes."""
+    import torch
+    from oracle.oracle_c import OracleXRS
+    stripe = 16 * size
+    ptr, buf = host_buf(n * stripe, True)
+    dptr = xrs_amd.lib().xrs_host_device_pointer(ptr)
+    assert dptr, "no device mapping"
+    buf[:] = np.random.default_rng(3).integers(0, 256, size=n * stripe, dtype=np.uint8)
+    x = xrs_amd.XRS(D, P)
+    x.encode_batched(dptr, size, size, stripe, n, 0)
+    torch.cuda.synchronize()
+    o = OracleXRS(D, P)
+    for s in range(min(n, 4)):
+        v = [buf[s * stripe + i * size: s * stripe + (i + 1) * size].copy() for i in range(16)]
+        w = [r.copy() for r in v]
+        o.encode(w)
+        assert all(np.array_equal(a, b) for a, b in zip(v, w)), s
+    fn = ((lambda i: x.encode_batched(dptr, size, size, stripe, n, 0)) if op == "encode" else
+          (lambda i: x.reconst_one_batched(dptr, size, size, stripe, n, i % D, 0)))
+    fn(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        fn(i)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    algo = n * (16 if op == "encode" else 9) * size
+    h2d = n * (D if op == "encode" else 8) * size
+    d2h = n * (P if op == "encode" else 1) * size
+    xrs_amd.lib().xrs_host_free(ptr)
+    return {"op": op, "vect_bytes": size, "stripes": n, "pinned": True, "mode": "zero-copy kernel",
+            "ms": round(dt * 1e3, 3), "algorithmic_gibps": round(algo / dt / 2**30, 2),
+            "h2d_gbs": round(h2d / dt / 1e9, 2), "d2h_gbs": round(d2h / dt / 1e9, 2)}
+
+
 def main():
-    for op, size, n in [("encode", 4096, 16384), ("encode", 1 << 20, 64),
-                        ("reconst_one", 1 << 20, 64), ("reconst_one", 4096, 16384)]:
-        for pinned in (True, False):
-            print(json.dumps(run(op, size, n, pinned, reps=5 if pinned else 2)), flush=True)
+    cases = [("encode", 4096, 16384), ("encode", 1 << 20, 64),
+             ("reconst_one", 1 << 20, 64), ("reconst_one", 4096, 16384)]
+    modes = sys.argv[1:] or ["pipeline", "zero-copy"]
+    for op, size, n in cases:
+        if "pipeline" in modes:
+            for pinned in (True, False):
+                print(json.dumps(run(op, size, n, pinned, reps=5 if pinned else 2)), flush=True)
+        if "zero-copy" in modes:
+            print(json.dumps(run_zero_copy(op, size, n, reps=5)), flush=True)
 
 
 if __name__ == "__main__":

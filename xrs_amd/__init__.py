@@ -91,6 +91,7 @@ def _load():
         "xrs_host_free": ([P], None),
         "xrs_host_register": ([P, Z], I),
         "xrs_host_unregister": ([P], I),
+        "xrs_host_device_pointer": ([P], P),
         "xrs_encode_shards": ([P, PP, Z, Z, Z, P], I),
         "xrs_reconst_one_shards": ([P, PP, Z, Z, Z, I, P], I),
         "xrs_reconst_shards": ([P, PP, Z, Z, Z, IP, I, IP, I, P], I),

@@ -1101,15 +1101,20 @@ int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, si
 
 void* xrs_host_alloc(size_t bytes) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped) != hipSuccess) return nullptr;
   return p;
+}
+void* xrs_host_device_pointer(void* host) {
+  void* d = nullptr;
+  if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  return d;
 }
 void xrs_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 int xrs_host_register(void* p, size_t bytes) {
   if (!p || !bytes) return XRS_ERR_INVALID_ARG;
-  return hip_err(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return hip_err(hipHostRegister(p, bytes, hipHostRegisterMapped));
 }
 int xrs_host_unregister(void* p) {
   if (!p) return XRS_ERR_INVALID_ARG;

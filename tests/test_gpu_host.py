@@ -23,8 +23,13 @@ def pinned(nbytes):
 
 
 @pytest.mark.parametrize("size,n", [(4096, 5000), (1 << 20, 70), (1026, 333), (8 << 20, 9)])
-@pytest.mark.parametrize("pin", [True, False])
-def test_encode_host_vs_oracle(rng, size, n, pin):
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
+def test_encode_host_vs_oracle(rng, monkeypatch, size, n, mode):
+    """Pinned memory runs the kernels in place over PCIe (zero copy) unless
+    XRS_HOST_ZC=0 selects the copy pipeline; pageable memory always copies."""
+    pin = mode != "pageable"
+    if mode == "pinned_dma":
+        monkeypatch.setenv("XRS_HOST_ZC", "0")
     stripe = 16 * size
     if pin:
         ptr, buf = pinned(n * stripe)
@@ -72,3 +77,25 @@ def test_encode_host_padded_layout(rng):
         for s in range(n):
             mask[s * stripe + i * shard:s * stripe + i * shard + size] = False
     assert np.array_equal(buf[mask], orig[mask])  # only parity bytes written
+
+
+def test_host_zero_copy_inside_allocation(rng):
+    """A batch that starts inside a pinned allocation, with a padded layout:
+    the in-place path addresses it through the mapped device pointer."""
+    size, n = 4096, 700
+    shard, stripe = size + 64, 16 * (size + 64) + 128
+    ptr, buf = pinned(n * stripe + 8192)
+    off = 4096
+    buf[:] = rng.integers(0, 256, size=len(buf), dtype=np.uint8)
+    orig = buf.copy()
+    x = xrs_amd.XRS(D, P)
+    x.encode_host(ptr + off, size, shard, stripe, n)
+    o = OracleXRS(D, P)
+    for s in (0, 1, 345, n - 1):
+        v = [orig[off + s * stripe + i * shard:][:size].copy() for i in range(16)]
+        o.encode(v)
+        for i in range(16):
+            a = off + s * stripe + i * shard
+            assert np.array_equal(buf[a:a + size], v[i]), (s, i)
+    assert xrs_amd.lib().xrs_host_device_pointer(ptr)
+    xrs_amd.lib().xrs_host_free(ptr)

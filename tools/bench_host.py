@@ -96,8 +96,12 @@ def main():
     modes = sys.argv[1:] or ["pipeline", "zero-copy"]
     for op, size, n in cases:
         if "pipeline" in modes:
-            for pinned in (True, False):
-                print(json.dumps(run(op, size, n, pinned, reps=5 if pinned else 2)), flush=True)
+            for pinned, zc in ((True, "1"), (True, "0"), (False, "0")):
+                os.environ["XRS_HOST_ZC"] = zc  # pinned: in place (1) or copy pipeline (0)
+                r = run(op, size, n, pinned, reps=5 if pinned else 2)
+                r["mode"] = "in place (zero copy)" if pinned and zc == "1" else "copy pipeline"
+                print(json.dumps(r), flush=True)
+            os.environ.pop("XRS_HOST_ZC", None)
         if "zero-copy" in modes:
             print(json.dumps(run_zero_copy(op, size, n, reps=5)), flush=True)
 

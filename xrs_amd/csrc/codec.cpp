@@ -894,8 +894,10 @@ int xrs_get_need_vects(const xrs_codec* x, int k, int* a_need, int* a_len, int b
 // 4 KiB + 256 B pad.
 int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* stripe_stride) {
   if (!shard_stride || !stripe_stride || n_shards < 1) return XRS_ERR_INVALID_ARG;
-  size_t pad = 0;
-  if (size > (64u << 10)) pad = size >= (4u << 20) ? 4096 + 256 : 256;
+  // With the XCD-aware block order (kernels.hip) back-to-back shards stream
+  // as fast as padded ones below 4 MiB; 8 MiB Encode still gains ~3% from a
+  // 4 KiB + 256 B pad (profiles/r01_order_ab.log).
+  const size_t pad = size >= (4u << 20) ? 4096 + 256 : 0;
   const size_t s = (size + 15) / 16 * 16 + pad;
   *shard_stride = s;
   *stripe_stride = s * static_cast<size_t>(n_shards);
@@ -1067,12 +1069,19 @@ namespace {
 uint8_t* host_zero_copy(uint8_t* host_base, size_t extent) {
   const char* v = std::getenv("XRS_HOST_ZC");
   if (v && v[0] == '0') return nullptr;
+  // A failed probe (pageable memory) leaves the runtime's last-error set;
+  // clear it, or the next launch's hipGetLastError() reports it.
   void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, host_base, 0) != hipSuccess || !d) return nullptr;
+  if (hipHostGetDevicePointer(&d, host_base, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   hipDeviceptr_t base = nullptr;
   size_t len = 0;
-  if (hipMemGetAddressRange(&base, &len, static_cast<hipDeviceptr_t>(d)) != hipSuccess || !base)
+  if (hipMemGetAddressRange(&base, &len, static_cast<hipDeviceptr_t>(d)) != hipSuccess || !base) {
+    (void)hipGetLastError();
     return nullptr;
+  }
   const uintptr_t lo = reinterpret_cast<uintptr_t>(base), p0 = reinterpret_cast<uintptr_t>(d);
   if (p0 < lo || p0 + extent > lo + len) return nullptr;
   return static_cast<uint8_t*>(d);
@@ -1156,7 +1165,11 @@ void* xrs_host_alloc(size_t bytes) {
 }
 void* xrs_host_device_pointer(void* host) {
   void* d = nullptr;
-  if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  if (!host) return nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+    (void)hipGetLastError();  // not mapped: do not leave the error for the next launch
+    return nullptr;
+  }
   return d;
 }
 void xrs_host_free(void* p) {

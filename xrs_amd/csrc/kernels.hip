@@ -33,6 +33,7 @@ namespace {
 
 constexpr int kDyn = -1;  // count known only at run time
 constexpr int kBlock = 256;
+constexpr uint64_t kMaxBlocks = 0x7fffffffu;  // 1-D grid limit
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Global (address space 1) views: global_load/store instead of flat_*.
@@ -102,6 +103,30 @@ __device__ __forceinline__ uint64_t row_addr(const RowRef& r, uint64_t stripe, u
   return r.ptr + stripe * r.stripe_stride + off;
 }
 
+// ---- XCD-aware block order -------------------------------------------------
+// The dispatcher hands block i to XCD i % 8 (MI355X: 8 XCDs x 32 CUs, one L2
+// each).  Block order maps hardware block b to the logical block it works on:
+// groups of 8*K logical blocks, each XCD taking K consecutive ones, so every
+// XCD streams contiguous pieces of the batch instead of every 8th 4 KiB piece.
+// K = 0 keeps the plain order.  Blocks past the last whole group keep their
+// own index, so the map is a bijection on [0, nblk) for any K.  Measured on
+// MI355X (tools/mapprobe.hip, profiles/r01_mapprobe3.log): Encode 8 MiB
+// unpadded 4.06 -> 5.99 TB/s, ReconstOne 1 MiB unpadded 5.13 -> 5.89 TB/s,
+// Encode 4 KiB 5.79 -> 6.02 TB/s, ReconstOne 4 KiB 6.10 -> 6.36 TB/s.
+struct BlockOrder {
+  uint32_t nblk;  // blocks in the grid
+  uint32_t k;     // logical blocks per XCD per group; 0: plain order
+};
+
+__device__ __forceinline__ uint64_t logical_block(const BlockOrder& o) {
+  const uint32_t b = blockIdx.x;
+  if (o.k == 0) return b;
+  const uint32_t q = b >> 3, g = q / o.k;
+  const uint64_t span = 8ull * o.k;
+  if ((g + 1) * span > o.nblk) return b;
+  return g * span + (b & 7u) * static_cast<uint64_t>(o.k) + (q - g * o.k);
+}
+
 // ============================================================ pair kernel
 // Encode / Replace / Update:  for o in [0, H):
 //   dst_r[o]   (^)= sum_c coef[c][r] * src_c[o]
@@ -114,6 +139,7 @@ struct PairArgs {
   RowRef dst[P];
   uint32_t pbmask[P];  // bit c: XOR src_c's a-half into dst_r's b-half
   int n_src;
+  BlockOrder order;
   uint64_t half;    // H
   uint64_t chunks;  // lanes per stripe
   uint64_t total;   // n_stripes * chunks
@@ -182,7 +208,7 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
 template <int P, int C, bool ACC, bool VEC>
 __global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
@@ -270,6 +296,7 @@ struct RowsArgs {
   uint32_t xmask[XM];
   RowRef dst[R];
   int nm, nx;
+  BlockOrder order;
   uint64_t len;
   uint64_t chunks;
   uint64_t total;
@@ -315,7 +342,7 @@ __device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, c
 template <int R, int NM, int NX, bool ACC, bool VEC>
 __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
@@ -386,6 +413,7 @@ struct StagedArgs {
   int rb[kStOut];          // ... and their b-row indexes
   uint32_t bstore;
   int nd, na, nb, nl, nn, nr;
+  BlockOrder order;
   uint64_t half, chunks, total;
 };
 
@@ -409,7 +437,7 @@ template <int NL, int NN, bool VEC>
 __global__ __launch_bounds__(kBlock) void staged_kernel(const StagedArgs<NL, NN, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
   constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
@@ -479,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   const int nd = a.nd;
   constexpr int W = VEC ? 4 : 1;
   constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
@@ -548,6 +576,35 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
+enum class Shape { kPair, kRows, kStaged };
+
+// K per kernel shape and half-vect length, from interleaved medians of every
+// order on MI355X (profiles/r01_mapprobe2.log, r01_mapprobe3.log):
+//  * pair (Encode/Update/Replace): K = 32 is best or within 1% at 4 KiB-8 MiB;
+//  * rows (ReconstOne): 4 KiB vects want one range per XCD (K = nblk/8),
+//    8-128 KiB vects the plain order, >= 512 KiB vects K = 128;
+//  * staged (general Reconst) reads both halves of every shard like pair.
+// The byte-granular (!VEC) path keeps the plain order.  XRS_BLOCK_ORDER=<K>
+// overrides (0: plain order; "full": one range per XCD) for A/B runs.
+BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
+  BlockOrder o{static_cast<uint32_t>(blocks), 0};
+  if (!vec) return o;
+  if (const char* e = std::getenv("XRS_BLOCK_ORDER")) {
+    if (std::strcmp(e, "full") == 0) o.k = static_cast<uint32_t>(blocks / 8);
+    else o.k = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+    return o;
+  }
+  switch (shape) {
+    case Shape::kPair:
+    case Shape::kStaged: o.k = 32; break;
+    case Shape::kRows:
+      if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
+      else if (len >= (256u << 10)) o.k = 128;
+      break;
+  }
+  return o;
+}
+
 template <int NL, int NN, bool VEC>
 int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   StagedArgs<NL, NN, VEC> a;
@@ -591,6 +648,9 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kStaged, VEC, p.half, blocks);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
   // (A compile-time survivor count, ND = 12, let the scheduler hoist the
   // b-row loads: 225-232 VGPRs plus scratch.  Runtime nd only.)
   if (late)
@@ -639,6 +699,9 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kPair, VEC, p.half, blocks);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
   hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());
@@ -684,6 +747,9 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kRows, VEC, p.len, blocks);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
   hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());

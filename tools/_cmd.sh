@@ -1,8 +1,5 @@
 set -u
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 400 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1; rc=$?; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || exit $?
-bash tools/gpu_pmc.sh > gpurun_out/pmc.log 2>&1; rc=$?; tail -20 gpurun_out/pmc.log; exit $rc
+timeout -k 10 200 tools/kbench rw > gpurun_out/kbench_rw.log 2>&1 || exit $?
+timeout -k 10 200 tools/kbench rw xcd > gpurun_out/kbench_rw_xcd.log 2>&1 || exit $?
+cat gpurun_out/kbench_rw.log gpurun_out/kbench_rw_xcd.log

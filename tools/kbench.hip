@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void read_glds(const u32x4* __restrict__ a, ui
 // ReconstOne / Encode address patterns split into their read and write parts.
 template <bool READ, bool WRITE>
 __global__ __launch_bounds__(256) void r1_rw(const RowsArgs<2, 12, 4, true> a, uint32_t* sink) {
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * 256 + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * 16;
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void r1_rw(const RowsArgs<2, 12, 4, true> a, u
 
 template <bool READ, bool WRITE>
 __global__ __launch_bounds__(256) void enc_rw(const PairArgs<4, 12, true> a, uint32_t* sink) {
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * 256 + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = (gid - stripe * a.chunks) * 16;
@@ -773,8 +773,10 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (which == "rw") {
-    // same setup as "gs": ReconstOne 1 MiB pad 256, Encode 4 KiB pad 0
-    const uint64_t S1 = 1 << 20, n1 = 256, H1 = S1 / 2, sh1 = S1 + 256, st1 = 16 * sh1;
+    // same setup as "gs": ReconstOne 1 MiB pad 256, Encode 4 KiB pad 0;
+    // "rw xcd": ReconstOne 1 MiB unpadded, both in the product's XCD block order
+    const bool xcd = argc > 2 && std::string(argv[2]) == "xcd";
+    const uint64_t S1 = 1 << 20, n1 = 256, H1 = S1 / 2, sh1 = S1 + (xcd ? 0 : 256), st1 = 16 * sh1;
     const uint64_t S2 = 4096, n2 = 65536, H2 = S2 / 2, st2 = 16 * S2;
     uint8_t *b1, *b2;
     uint32_t* sink;
@@ -805,6 +807,10 @@ int main(int argc, char** argv) {
     for (int r = 0; r < 4; ++r) pa.dst[r] = {base2 + (12 + r) * S2, st2};
     pa.n_src = 12; pa.half = H2; pa.chunks = H2 / 16; pa.total = pa.chunks * n2;
     const unsigned bl1 = (unsigned)(ra.total / 256), bl2 = (unsigned)(pa.total / 256);
+    if (xcd) {
+      ra.order = {bl1, 128};
+      pa.order = {bl2, 32};
+    }
     std::vector<double> t[8];
     for (int round = 0; round < 5; ++round) {
       t[0].push_back(tm.ms([&] { hipLaunchKernelGGL((rows_kernel<2, 12, 4, false, true>), dim3(bl1), dim3(256), 0, 0, ra); }, 5));

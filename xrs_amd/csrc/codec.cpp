@@ -888,10 +888,6 @@ int xrs_get_need_vects(const xrs_codec* x, int k, int* a_need, int* a_len, int b
 }
 
 // ---------------------------------------------------------------- batched
-// Pads measured with tools/kbench.hip (padab, interleaved medians, 4 GiB
-// batches): <= 64 KiB vects stream best back to back; 1 MiB vects lose 9% on
-// ReconstOne without a 256 B pad; 8 MiB vects lose 30% on Encode without a
-// 4 KiB + 256 B pad.
 int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* stripe_stride) {
   if (!shard_stride || !stripe_stride || n_shards < 1) return XRS_ERR_INVALID_ARG;
   // With the XCD-aware block order (kernels.hip) back-to-back shards stream

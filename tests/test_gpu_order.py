@@ -46,11 +46,14 @@ def test_encode_and_reconst_one_every_order(rng, monkeypatch, order, size, n):
     assert np.array_equal(t.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("variant", ["late", "0"])
 @pytest.mark.parametrize("order", ["0", "32", "full"])
 @pytest.mark.parametrize("size,n", [(4096, 513), (1 << 20, 9)])
-def test_staged_reconst_every_order(rng, monkeypatch, order, size, n):
-    """Three lost data vects through the staged kernel, side effects included."""
+def test_staged_reconst_every_order(rng, monkeypatch, variant, order, size, n):
+    """Three lost data vects through every staged kernel variant, side effects
+    included."""
     monkeypatch.setenv("XRS_BLOCK_ORDER", order)
+    monkeypatch.setenv("XRS_STAGED_LATE", variant)
     host, t = batch(rng, size, n)
     o = OracleXRS(D, P)
     o.encode_batch(host, size, n)

@@ -175,6 +175,10 @@ void xrs_queue_free(xrs_queue *q);
 int xrs_queue_encode(xrs_queue *q, uint8_t *const *vects, int n);
 int xrs_queue_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k);
 size_t xrs_queue_batch_stripes(const xrs_queue *q);
+/* Counters since xrs_queue_new: out[0] batches run, out[1] stripes run,
+ * out[2] ns from each batch's launch to its completion, out[3] ns each batch
+ * waited between opening and launch (summed over batches). */
+int xrs_queue_stats(xrs_queue *q, uint64_t out[4]);
 
 #ifdef __cplusplus
 }

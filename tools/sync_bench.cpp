@@ -78,9 +78,15 @@ int main(int argc, char** argv) {
     stop = true;
     for (auto& x : th) x.join();
     const double dt = now() - t0;
+    uint64_t st[4] = {0, 0, 0, 0};
+    xrs_queue_stats(q, st);
+    const double nb = st[0] ? static_cast<double>(st[0]) : 1.0;
     std::printf("{\"api\": \"xrs_queue_encode\", \"vect_bytes\": %zu, \"threads\": %d, "
-                "\"stripes_per_s\": %.0f, \"gibps\": %.3f}\n", size, threads, total / dt,
-                total * 16.0 * size / dt / (1 << 30));
+                "\"stripes_per_s\": %.0f, \"gibps\": %.3f, \"batches\": %llu, "
+                "\"stripes_per_batch\": %.1f, \"run_us_per_batch\": %.1f, "
+                "\"wait_us_per_batch\": %.1f}\n", size, threads, total / dt,
+                total * 16.0 * size / dt / (1 << 30), (unsigned long long)st[0], st[1] / nb,
+                st[2] / nb / 1e3, st[3] / nb / 1e3);
     std::fflush(stdout);
     xrs_queue_free(q);
   }

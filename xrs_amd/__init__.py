@@ -101,6 +101,7 @@ def _load():
         "xrs_queue_encode": ([P, PP, I], I),
         "xrs_queue_reconst_one": ([P, PP, I, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
+        "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -339,3 +340,9 @@ class XRSQueue:
     def reconst_one(self, vects, need_reconst: int) -> None:
         _raise(_lib.xrs_queue_reconst_one(self._h, _ptrs(vects), len(vects), int(need_reconst)),
                need_reconst)
+
+    def stats(self) -> dict:
+        """Batches and stripes run so far, and summed device / queueing ns."""
+        out = (ctypes.c_uint64 * 4)()
+        _raise(_lib.xrs_queue_stats(self._h, out))
+        return {"batches": out[0], "stripes": out[1], "run_ns": out[2], "wait_ns": out[3]}

@@ -76,6 +76,10 @@ struct xrs_queue {
   int open = -1;
   int running = 0;  // batches being run by workers
   bool stop = false;
+  // statistics (guarded by mu): batches run, stripes run, device time
+  // (launch to stream sync) and queueing time (open to launch) summed over
+  // batches, in ns
+  uint64_t st_batches = 0, st_stripes = 0, st_run_ns = 0, st_wait_ns = 0;
   std::mutex mu;
   std::condition_variable cv_work, cv_free;
   std::thread worker[kWorkers];
@@ -147,10 +151,20 @@ void xrs_queue::work() {
     }
     b[pick].state = RUNNING;
     ++running;
+    const size_t n = b[pick].reserved;
+    const auto t0 = Clock::now();
+    const uint64_t waited =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - b[pick].opened).count();
     lk.unlock();
     run(pick);
+    const uint64_t ran =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
     lk.lock();
     --running;
+    ++st_batches;
+    st_stripes += n;
+    st_run_ns += ran;
+    st_wait_ns += waited;
   }
 }
 
@@ -326,5 +340,15 @@ int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
 }
 
 size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }
+
+int xrs_queue_stats(xrs_queue* q, uint64_t out[4]) {
+  if (!q || !out) return XRS_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(q->mu);
+  out[0] = q->st_batches;
+  out[1] = q->st_stripes;
+  out[2] = q->st_run_ns;
+  out[3] = q->st_wait_ns;
+  return XRS_OK;
+}
 
 }  // extern "C"

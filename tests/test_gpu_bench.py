@@ -1,0 +1,55 @@
+"""GPU tests of bench.py's driver contract: one JSON line with the required
+keys, at N=1 and at N=2 (two ranks through torch.distributed.run; on the
+one-GPU box they share cuda:0 over gloo, as XRS_DIST_BACKEND=gloo selects —
+the driver's multi-GPU runs use nccl, one rank per GPU)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "3", "--warmup", "1", "--enc-stripes", "2048", "--rec-stripes", "16",
+         "--no-cpu-baseline"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
+        "cpu_baseline"}
+
+
+def _line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_one_gpu_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL,
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _line(r.stdout)
+    assert KEYS <= set(j)
+    assert j["n_gpus"] == 1 and j["steps"] == 3 and j["value"] > 0
+    assert j["roofline"]["bound"] == "hbm" and 0 < j["roofline"]["frac"] < 1
+    assert set(j["kernels"]) == {"encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m"}
+
+
+def test_bench_two_ranks_contract():
+    env = dict(os.environ, XRS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _line(r.stdout)
+    assert KEYS <= set(j)
+    assert j["n_gpus"] == 2 and j["scaling"] == "weak" and j["value"] > 0
+    assert j["cpu_baseline"] is None  # rank 0 at N=1 only

@@ -399,3 +399,33 @@ def test_update_linearity_full_size(cuda):
     assert torch.equal(v[:, D:], par1)
     del t, v, par0, par1, new
     torch.cuda.empty_cache()
+
+
+def test_config5_per_gpu_share_round_trip(cuda):
+    """BASELINE config 5's per-GPU share at full size: 8,192 stripes of 12+4
+    1 MiB vects (128 GiB) resident on one GPU.  Encode, check sampled stripes
+    against the oracle, erase data shard k of every stripe and ReconstOne it
+    back bit for bit."""
+    size, n = 1 << 20, 8192
+    S = 16 * size
+    free, _ = torch.cuda.mem_get_info(cuda)
+    if free < n * S + n * size + (8 << 30):
+        pytest.skip("needs ~145 GiB of free HBM")
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    t = _dev_random(n * S, cuda, 5)
+    x.encode_batched(t.data_ptr(), size, size, S, n, stream())
+    torch.cuda.synchronize()
+    v = t.view(n, 16, size)
+    for s in (0, 4097, n - 1):
+        host = v[s].cpu().numpy().copy()
+        ref = [host[i].copy() for i in range(16)]
+        o.encode(ref)
+        assert np.array_equal(host, np.stack(ref)), s
+    k = 10
+    keep = v[:, k].clone()
+    v[:, k].fill_(0)
+    x.reconst_one_batched(t.data_ptr(), size, size, S, n, k, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(v[:, k], keep)
+    del t, v, keep
+    torch.cuda.empty_cache()

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Sweep XRS_BLOCK_ORDER over the four headline launches through the product
+launchers (interleaved rounds, median per K).  Prints one JSON line per
+(launch, K); "default" is the library's own choice."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import xrs_amd  # noqa: E402
+
+D, P = 12, 4
+ROUNDS = int(os.environ.get("ROUNDS", "11"))
+ORDERS = [None, "0", "16", "32", "64", "128", "256", "1024", "full"]
+
+
+def time_ms(fn, reps=4):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    x = xrs_amd.XRS(D, P)
+    s = torch.cuda.current_stream().cuda_stream
+    cases = []
+    for size, n in ((4096, 65536), (1 << 20, 512)):
+        shard, stripe = xrs_amd.batch_strides(size, D + P)
+        buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
+        base = buf.data_ptr()
+        cases.append((f"encode_{size}", 16 * size * n, buf,
+                      lambda b=base, sz=size, sh=shard, st=stripe, nn=n:
+                      x.encode_batched(b, sz, sh, st, nn, s)))
+        cases.append((f"reconst_one_{size}", 9 * size * n, buf,
+                      lambda b=base, sz=size, sh=shard, st=stripe, nn=n:
+                      x.reconst_one_batched(b, sz, sh, st, nn, 3, s)))
+    t = {(c[0], o): [] for c in cases for o in ORDERS}
+    for _ in range(ROUNDS):
+        for name, _, _, fn in cases:
+            for o in ORDERS:
+                if o is None:
+                    os.environ.pop("XRS_BLOCK_ORDER", None)
+                else:
+                    os.environ["XRS_BLOCK_ORDER"] = o
+                t[(name, o)].append(time_ms(fn))
+    os.environ.pop("XRS_BLOCK_ORDER", None)
+    for name, nbytes, _, _ in cases:
+        for o in ORDERS:
+            med = sorted(t[(name, o)])[ROUNDS // 2]
+            print(json.dumps({"launch": name, "order": o or "default",
+                              "gbs": round(nbytes / med / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

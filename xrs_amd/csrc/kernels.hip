@@ -582,7 +582,8 @@ enum class Shape { kPair, kRows, kStaged };
 // order on MI355X (profiles/r01_mapprobe2.log, r01_mapprobe3.log):
 //  * pair (Encode/Update/Replace): K = 32 is best or within 1% at 4 KiB-8 MiB;
 //  * rows (ReconstOne): 4 KiB vects want one range per XCD (K = nblk/8),
-//    8-128 KiB vects the plain order, >= 512 KiB vects K = 128;
+//    8-128 KiB vects the plain order, >= 512 KiB vects K = half / 8 KiB up
+//    to 256 (1 MiB: 64, 8 MiB: 256; profiles/r01_order_sweep.log);
 //  * staged (general Reconst) reads both halves of every shard like pair.
 // The byte-granular (!VEC) path keeps the plain order.  XRS_BLOCK_ORDER=<K>
 // overrides (0: plain order; "full": one range per XCD) for A/B runs.
@@ -599,7 +600,7 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
     case Shape::kStaged: o.k = 32; break;
     case Shape::kRows:
       if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
-      else if (len >= (256u << 10)) o.k = 128;
+      else if (len >= (256u << 10)) o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 13));
       break;
   }
   return o;

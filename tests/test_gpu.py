@@ -151,7 +151,7 @@ def test_replace_sync(cuda, rng, to_zero):
 
 
 @pytest.mark.parametrize("d,p", [(1, 2), (2, 3), (5, 5), (10, 4), (6, 3), (20, 8), (3, 9),
-                                 (30, 6), (100, 10)])
+                                 (30, 6), (100, 10), (200, 56), (250, 6)])
 def test_other_configs_sync(cuda, rng, d, p):
     """Runtime-shaped kernels, output groups (p > 4) and source chunks (d > 24)."""
     x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)

@@ -246,6 +246,9 @@ def main():
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom["achieved_gbs"] / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
+        # the north star's "HBM-read roofline": read bytes only over the same peak
+        "read_achieved": dom["read_only_gbs"],
+        "read_frac": round(dom["read_only_gbs"] / HBM_PEAK_GBS, 4),
     }
 
     cpu = None

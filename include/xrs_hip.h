@@ -139,18 +139,19 @@ int xrs_reconst_shards(const xrs_codec *codec, uint8_t *const *shards, size_t st
 /* Let kernels running on `device` access HBM of `peer` (idempotent). */
 int xrs_enable_peer_access(int device, int peer);
 
-/* ---- host-resident batches (pipelined, synchronous) -------------------- *
+/* ---- host-resident batches (synchronous) ------------------------------- *
  * The real caller's path (shards start and end in host memory, e.g. disk or
- * NIC buffers): stripes are moved in chunks through device slots on three
- * streams so H2D, kernel and D2H overlap.  Host layout as for *_batched.
- * Use pinned memory (xrs_host_alloc / xrs_host_register) for full PCIe rate;
- * pageable memory works but copies synchronously. */
+ * NIC buffers).  Host layout as for *_batched.  A batch inside pinned, mapped
+ * memory (xrs_host_alloc / xrs_host_register) runs in place: the kernels read
+ * and write it over PCIe.  Pageable memory (or XRS_HOST_ZC=0) is moved in
+ * chunks through device slots on three streams so H2D, kernel and D2H
+ * overlap. */
 int xrs_encode_host(const xrs_codec *codec, uint8_t *host_base, size_t size, size_t shard_stride,
                     size_t stripe_stride, size_t n_stripes);
 /* ReconstOne(k) per stripe; only the GetNeedVects halves cross PCIe. */
 int xrs_reconst_one_host(const xrs_codec *codec, uint8_t *host_base, size_t size,
                          size_t shard_stride, size_t stripe_stride, size_t n_stripes, int k);
-void *xrs_host_alloc(size_t bytes);           /* pinned, device-mapped host memory (NULL on failure) */
+void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */
 void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */
 int xrs_host_unregister(void *p);
@@ -159,6 +160,24 @@ int xrs_host_unregister(void *p);
  * *_batched calls: the kernels then read and write host memory over PCIe
  * (zero copy). */
 void *xrs_host_device_pointer(void *host);
+
+/* ---- one process, several GPUs ----------------------------------------- *
+ * A group holds one codec per listed device.  Host-resident batches are split
+ * into contiguous stripe ranges, one per member, run concurrently (one host
+ * thread per GPU, each GPU on its own PCIe link); no data moves between GPUs.
+ * A device may be listed more than once.  Device-resident batches already on
+ * each GPU take the member codecs' *_batched calls directly. */
+typedef struct xrs_group xrs_group;
+int xrs_group_new(int data_num, int parity_num, const int *devices, int n_devices,
+                  xrs_group **out);
+void xrs_group_free(xrs_group *g);
+int xrs_group_size(const xrs_group *g);
+const xrs_codec *xrs_group_codec(const xrs_group *g, int i);
+int xrs_group_encode_host(xrs_group *g, uint8_t *host_base, size_t size, size_t shard_stride,
+                          size_t stripe_stride, size_t n_stripes);
+int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
+                               size_t shard_stride, size_t stripe_stride, size_t n_stripes,
+                               int k);
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling

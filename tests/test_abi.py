@@ -110,6 +110,8 @@ def test_compute_without_gpu_fails_loudly():
         x.encode([np.zeros(8, np.uint8) for _ in range(16)])
     with pytest.raises(xrs_amd.XRSError, match="no gpu device"):
         x.encode_batched(1 << 20, 4096, 4096, 65536, 1)
+    with pytest.raises(xrs_amd.XRSError, match="no gpu device"):
+        xrs_amd.XRSGroup(12, 4, [0])
 
 
 def test_single_hip_runtime():

@@ -1,0 +1,63 @@
+"""GPU tests of the one-process multi-GPU group (xrs_group_*): a host-resident
+batch split across members, against the oracle.  The box has one GPU, so the
+members are the same device listed more than once: the split, the threads and
+the per-member codecs are exercised; cross-device PCIe scaling is not."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+D, P = 12, 4
+
+
+def _pinned(nbytes):
+    p = xrs_amd.lib().xrs_host_alloc(nbytes)
+    assert p
+    return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("size,n", [(4096, 1001), (1 << 20, 7), (1026, 5)])
+def test_group_host_vs_oracle(rng, devices, pinned, size, n):
+    stripe = 16 * size
+    if pinned:
+        ptr, buf = _pinned(n * stripe)
+    else:
+        buf = np.empty(n * stripe, np.uint8)
+        ptr = buf.ctypes.data
+    buf[:] = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+    ref = buf.reshape(n, 16, size).copy()
+    OracleXRS(D, P).encode_batch(ref, size, n)
+    g = xrs_amd.XRSGroup(D, P, devices)
+    assert len(g) == len(devices)
+    g.encode_host(ptr, size, size, stripe, n)
+    v = buf.reshape(n, 16, size)
+    assert np.array_equal(v, ref)
+    k = 4
+    v[:, k] = 0
+    g.reconst_one_host(ptr, size, size, stripe, n, k)
+    assert np.array_equal(v, ref)
+    del g
+    if pinned:
+        xrs_amd.lib().xrs_host_free(ptr)
+
+
+def test_group_errors():
+    with pytest.raises(xrs_amd.XRSError, match="invalid argument"):
+        xrs_amd.XRSGroup(D, P, [])
+    with pytest.raises(xrs_amd.XRSError, match="invalid argument"):
+        xrs_amd.XRSGroup(D, P, [torch.cuda.device_count()])
+    with pytest.raises(xrs_amd.XRSError, match="illegal parity"):
+        xrs_amd.XRSGroup(D, 1, [0])
+    g = xrs_amd.XRSGroup(D, P, [0, 0])
+    buf = np.zeros(16 * 64, np.uint8)
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: 12$"):
+        g.reconst_one_host(buf.ctypes.data, 64, 64, 16 * 64, 1, 12)
+    with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 63$"):
+        g.encode_host(buf.ctypes.data, 63, 64, 16 * 64, 1)

@@ -90,6 +90,29 @@ def run_zero_copy(op, size, n, reps):
             "h2d_gbs": round(h2d / dt / 1e9, 2), "d2h_gbs": round(d2h / dt / 1e9, 2)}
 
 
+def run_group(op, size, n, devices, reps):
+    """xrs_group_*: the host batch split across `devices` (one PCIe link each),
+    pinned memory, kernels in place."""
+    stripe = 16 * size
+    ptr, buf = host_buf(n * stripe, True)
+    buf[:] = np.random.default_rng(3).integers(0, 256, size=n * stripe, dtype=np.uint8)
+    g = xrs_amd.XRSGroup(D, P, devices)
+    g.encode_host(ptr, size, size, stripe, n)
+    fn = ((lambda i: g.encode_host(ptr, size, size, stripe, n)) if op == "encode" else
+          (lambda i: g.reconst_one_host(ptr, size, size, stripe, n, i % D)))
+    fn(0)
+    t0 = time.perf_counter()
+    for i in range(reps):
+        fn(i)
+    dt = (time.perf_counter() - t0) / reps
+    algo = n * (16 if op == "encode" else 9) * size
+    del g
+    xrs_amd.lib().xrs_host_free(ptr)
+    return {"op": op, "vect_bytes": size, "stripes": n, "pinned": True,
+            "mode": f"group of {len(devices)} GPU(s) {devices}", "ms": round(dt * 1e3, 3),
+            "algorithmic_gibps": round(algo / dt / 2**30, 2)}
+
+
 def main():
     cases = [("encode", 4096, 16384), ("encode", 1 << 20, 64),
              ("reconst_one", 1 << 20, 64), ("reconst_one", 4096, 16384)]
@@ -104,6 +127,11 @@ def main():
             os.environ.pop("XRS_HOST_ZC", None)
         if "zero-copy" in modes:
             print(json.dumps(run_zero_copy(op, size, n, reps=5)), flush=True)
+        if "group" in modes:
+            import torch
+            ndev = torch.cuda.device_count()
+            for devs in ([0], list(range(ndev))) if ndev > 1 else ([0],):
+                print(json.dumps(run_group(op, size, n * len(devs), devs, reps=5)), flush=True)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-__all__ = ["XRS", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
+__all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
@@ -102,6 +102,12 @@ def _load():
         "xrs_queue_reconst_one": ([P, PP, I, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
+        "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
+        "xrs_group_free": ([P], None),
+        "xrs_group_size": ([P], I),
+        "xrs_group_codec": ([P, I], P),
+        "xrs_group_encode_host": ([P, P, Z, Z, Z, Z], I),
+        "xrs_group_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -308,6 +314,41 @@ class XRS:
                                       parity_shard_stride, parity_stripe_stride, n_stripes, stream)
         bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
+
+
+class XRSGroup:
+    """One process driving several GPUs (xrs_group_*): one codec per listed
+    device; host-resident batches are split into contiguous stripe ranges and
+    run concurrently, each GPU over its own PCIe link."""
+
+    def __init__(self, data_num: int, parity_num: int, devices):
+        devs = [int(d) for d in devices]
+        h = ctypes.c_void_p()
+        _raise(_lib.xrs_group_new(int(data_num), int(parity_num), _ints(devs), len(devs),
+                                  ctypes.byref(h)))
+        self._h = h
+        self.devices = devs
+        self.data_num = int(data_num)
+
+    def __del__(self, _free=_lib.xrs_group_free):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _free(h)
+            self._h = None
+
+    def __len__(self) -> int:
+        return _lib.xrs_group_size(self._h)
+
+    def encode_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                    n_stripes: int) -> None:
+        _raise(_lib.xrs_group_encode_host(self._h, host_base, size, shard_stride, stripe_stride,
+                                          n_stripes), size)
+
+    def reconst_one_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                         n_stripes: int, need_reconst: int) -> None:
+        rc = _lib.xrs_group_reconst_one_host(self._h, host_base, size, shard_stride,
+                                             stripe_stride, n_stripes, int(need_reconst))
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else need_reconst)
 
 
 class XRSQueue:

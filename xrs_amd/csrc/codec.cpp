@@ -1156,7 +1156,10 @@ int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, si
 
 void* xrs_host_alloc(size_t bytes) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped) != hipSuccess) return nullptr;
+  // Portable: pinned and mapped for every GPU, so one allocation can feed a
+  // group of devices (group.cpp).
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+    return nullptr;
   return p;
 }
 void* xrs_host_device_pointer(void* host) {
@@ -1173,7 +1176,7 @@ void xrs_host_free(void* p) {
 }
 int xrs_host_register(void* p, size_t bytes) {
   if (!p || !bytes) return XRS_ERR_INVALID_ARG;
-  return hip_err(hipHostRegister(p, bytes, hipHostRegisterMapped));
+  return hip_err(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
 }
 int xrs_host_unregister(void* p) {
   if (!p) return XRS_ERR_INVALID_ARG;

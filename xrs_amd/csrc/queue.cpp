@@ -8,7 +8,7 @@
 //   caller thread: reserve a slot in the open batch -> copy its vects into the
 //     batch's pinned staging (callers copy in parallel) -> wait -> copy its
 //     outputs back -> release the slot.
-//   worker threads (2): run a batch when it is full, or when it has waited
+//   worker threads (XRS_QUEUE_WORKERS, default 2): run a batch when it is full, or when it has waited
 //     max_wait_us with every reserved slot filled: one H2D of the whole batch,
 //     one kernel over all its stripes, one D2H, on the batch's own stream.
 //     Batches of up to XRS_QUEUE_ZC_MAX bytes (default 4 MiB) skip both
@@ -45,8 +45,8 @@ using Clock = std::chrono::steady_clock;
 
 namespace {
 
-constexpr int kBatches = 4;
-constexpr int kWorkers = 2;
+constexpr int kMaxWorkers = 8;  // batches in flight at once: XRS_QUEUE_WORKERS, default 2
+constexpr int kBatches = kMaxWorkers + 2;  // staging buffers: one per worker + two filling
 constexpr size_t kMaxBatchBytes = 64u << 20;
 
 enum State { FREE, OPEN, CLOSED, RUNNING, DONE };
@@ -82,7 +82,8 @@ struct xrs_queue {
   uint64_t st_batches = 0, st_stripes = 0, st_run_ns = 0, st_wait_ns = 0;
   std::mutex mu;
   std::condition_variable cv_work, cv_free;
-  std::thread worker[kWorkers];
+  std::thread worker[kMaxWorkers];
+  int n_workers = 2, n_batches = 4;
 
   void run(int i);
   void work();
@@ -126,7 +127,7 @@ void xrs_queue::work() {
   while (!stop) {
     int pick = -1;
     Clock::time_point next = Clock::now() + max_wait;
-    for (int i = 0; i < kBatches && pick < 0; ++i) {
+    for (int i = 0; i < n_batches && pick < 0; ++i) {
       Batch& bt = b[i];
       if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
       if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
@@ -206,7 +207,7 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
         cv_work.notify_all();
       }
       int f = -1;
-      for (int i = 0; i < kBatches && f < 0; ++i)
+      for (int i = 0; i < n_batches && f < 0; ++i)
         if (b[i].state == FREE) f = i;
       if (f < 0) {
         cv_free.wait(lk);
@@ -281,11 +282,15 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   q->max_wait = std::chrono::microseconds(max_wait_us);
   const char* zv = std::getenv("XRS_QUEUE_ZC_MAX");
   q->zc_max = (zv && *zv) ? static_cast<size_t>(std::strtoull(zv, nullptr, 0)) : (4u << 20);
+  const char* wv = std::getenv("XRS_QUEUE_WORKERS");
+  if (wv && *wv) q->n_workers = std::max(1, std::min(kMaxWorkers, std::atoi(wv)));
+  q->n_batches = q->n_workers + 2;
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
   int e = XRS_OK;
-  for (Batch& bt : q->b) {
+  for (int i = 0; i < q->n_batches; ++i) {
+    Batch& bt = q->b[i];
     if (hipHostMalloc(&bt.host, q->max_batch * q->stripe_bytes, hipHostMallocMapped) != hipSuccess ||
         hipMalloc(&bt.dev, q->max_batch * q->stripe_bytes) != hipSuccess ||
         hipStreamCreateWithFlags(&bt.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -300,7 +305,7 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     xrs_queue_free(q);
     return e;
   }
-  for (auto& w : q->worker) w = std::thread([q] { q->work(); });
+  for (int i = 0; i < q->n_workers; ++i) q->worker[i] = std::thread([q] { q->work(); });
   *out = q;
   return XRS_OK;
 }

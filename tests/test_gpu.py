@@ -192,6 +192,40 @@ def test_other_configs_sync(cuda, rng, d, p):
         assert all(np.array_equal(a, b) for a, b in zip(p1, p2))
 
 
+@pytest.mark.parametrize("grouped", ["0", "1"])
+@pytest.mark.parametrize("d,p", [(10, 4), (5, 5), (30, 6)])
+def test_rows_runtime_loops(cuda, rng, monkeypatch, grouped, d, p):
+    """Both loops of the runtime-count rows kernel (grouped loads: chosen for
+    grids under one block per CU; one row at a time: larger grids), forced
+    either way, on single stripes and on a batch: ReconstOne and the
+    step-by-step Reconst plan, side effects included."""
+    monkeypatch.setenv("XRS_ROWS_GROUPED", grouped)
+    monkeypatch.setenv("XRS_RECONST", "steps")
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    for size in (34, 4096):
+        v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d + p)]
+        o.encode(v)
+        a = [r.copy() for r in v]
+        a[1][:] = 0
+        x.reconst_one(a, 1)
+        assert np.array_equal(a[1], v[1])
+        lost = [int(t) for t in rng.permutation(d + p)[:p]]
+        has = [i for i in range(d + p) if i not in lost]
+        a1, a2 = [r.copy() for r in v], [r.copy() for r in v]
+        x.reconst(a1, has, lost)
+        o.reconst(a2, has, lost)
+        assert all(np.array_equal(s, t) for s, t in zip(a1, a2)), size
+    size, n = 4096, 300
+    host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    t = torch.from_numpy(host).cuda()
+    t[:, 2].zero_()
+    s = torch.cuda.current_stream().cuda_stream
+    x.reconst_one_batched(t.data_ptr(), size, size, (d + p) * size, n, 2, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), host)
+
+
 def test_errors_on_gpu(cuda):
     x = xrs_amd.XRS(D, P)
     with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 9$"):

@@ -81,12 +81,14 @@ def test_cpp_port_under_host_asan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.fixture(params=["staged", "staged_early", "stepwise"])
+@pytest.fixture(params=["staged", "staged_early", "staged_late", "stepwise"])
 def reconst_mode(request, monkeypatch):
     monkeypatch.delenv("XRS_RECONST", raising=False)
     monkeypatch.delenv("XRS_STAGED_LATE", raising=False)
     if request.param == "staged_early":
         monkeypatch.setenv("XRS_STAGED_LATE", "0")
+    elif request.param == "staged_late":
+        monkeypatch.setenv("XRS_STAGED_LATE", "1")
     elif request.param == "stepwise":
         monkeypatch.setenv("XRS_RECONST", "steps")
     return request.param

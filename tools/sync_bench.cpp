@@ -18,11 +18,79 @@ static double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// `sync_bench ref`: every sub-benchmark of the reference's xrs_test.go
+// (:471-680) as a per-stripe synchronous call on host vects, one thread, the
+// way `go test -bench` runs it (one stripe, b.N calls), with its SetBytes.
+static int ref_mode(xrs_codec* c) {
+  constexpr int d = 12, p = 4;
+  auto run = [](const char* name, size_t size, double bytes, auto&& call) {
+    if (call()) std::exit(3);
+    long n = 0;
+    const double t0 = now();
+    while (now() - t0 < 1.0) {
+      if (call()) std::exit(3);
+      ++n;
+    }
+    const double dt = (now() - t0) / n;
+    std::printf("{\"bench\": \"%s\", \"vect_bytes\": %zu, \"ns_per_op\": %.0f, \"MB_s\": %.1f}\n",
+                name, size, dt * 1e9, bytes / dt / 1e6);
+    std::fflush(stdout);
+  };
+  auto vects = [](size_t size) {
+    std::vector<std::vector<uint8_t>> v(d + p, std::vector<uint8_t>(size));
+    uint32_t s = 0x5EED;
+    for (int j = 0; j < d; ++j)
+      for (auto& b : v[j]) b = static_cast<uint8_t>((s = s * 1664525u + 1013904223u) >> 24);
+    return v;
+  };
+  char name[128];
+  for (size_t size : {size_t(4) << 10, size_t(1) << 20, size_t(8) << 20}) {
+    auto v = vects(size);
+    std::vector<uint8_t*> ptr;
+    for (auto& x : v) ptr.push_back(x.data());
+    std::snprintf(name, sizeof name, "BenchmarkXRS_Encode/(12+4)-%s",
+                  size < (1u << 20) ? "4KB" : size == (1u << 20) ? "1MB" : "8MB");
+    run(name, size, double(d + p) * size, [&] { return xrs_encode(c, ptr.data(), d + p, size); });
+  }
+  const size_t size = 4096;
+  auto v = vects(size);
+  std::vector<uint8_t*> ptr;
+  for (auto& x : v) ptr.push_back(x.data());
+  if (xrs_encode(c, ptr.data(), d + p, size)) return 3;
+  for (int i = 1; i <= p; ++i) {
+    std::vector<int> lost, has;
+    for (int j = 0; j < d + p; ++j) (j < i ? lost : has).push_back(j);
+    const double bytes = i == 1 ? (d - 1 + 2 + 3) * size / 2.0 + size : double(d + i) * size;
+    std::snprintf(name, sizeof name, "BenchmarkXRS_Reconst/(12+4)-4KB-reconst_%d_data_vects", i);
+    run(name, size, bytes, [&] {
+      return xrs_reconst(c, ptr.data(), d + p, size, has.data(), static_cast<int>(has.size()),
+                         lost.data(), i);
+    });
+  }
+  std::vector<uint8_t> nd(size, 0x5a);
+  run("BenchmarkXRS_Update/(12+4)-4KB", size, double(2 * p + 2) * size,
+      [&] { return xrs_update(c, ptr[5], nd.data(), size, 5, ptr.data() + d, p); });
+  for (int n = 1; n <= d - p; ++n) {
+    std::vector<int> rows;
+    for (int j = 0; j < n; ++j) rows.push_back(j);
+    std::snprintf(name, sizeof name, "BenchmarkXRS_Replace/(12+4)-4KB-replace_%d_data_vects", n);
+    run(name, size, double(n + 2 * p) * size,
+        [&] { return xrs_replace(c, ptr.data(), rows.data(), n, size, ptr.data() + d, p); });
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
   const int seconds = 2;
   xrs_codec* c = nullptr;
   if (xrs_new(12, 4, &c)) return 2;
+  if (argc > 1 && std::strcmp(argv[1], "ref") == 0) {
+    const int rc = ref_mode(c);
+    xrs_free(c);
+    std::fflush(stdout);
+    std::_Exit(rc);
+  }
+  const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
   // --- plain sync calls, one thread
   {
     std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, 1));

@@ -34,6 +34,7 @@ namespace {
 constexpr int kDyn = -1;  // count known only at run time
 constexpr int kBlock = 256;
 constexpr uint64_t kMaxBlocks = 0x7fffffffu;  // 1-D grid limit
+constexpr uint64_t kLatencyGrid = 256;         // blocks: one per CU (MI355X: 256 CUs)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Global (address space 1) views: global_load/store instead of flat_*.
@@ -296,6 +297,7 @@ struct RowsArgs {
   uint32_t xmask[XM];
   RowRef dst[R];
   int nm, nx;
+  int grouped;  // runtime counts: issue loads in groups (small grids)
   BlockOrder order;
   uint64_t len;
   uint64_t chunks;
@@ -375,9 +377,32 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
     if constexpr (NM & 1) rows_mac1<R, W>(acc, a.tab[NM - 1], xm[NM - 1]);
 #pragma unroll
     for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
+  } else if (a.grouped) {
+    // Runtime counts, small grid (latency-bound): groups of kGrp rows, each
+    // group's loads issued together, so a launch pays ceil(rows / kGrp)
+    // memory round trips instead of one per row.
+    constexpr int kGrp = 8;
+    for (int m0 = 0; m0 < a.nm; m0 += kGrp) {
+      uint32_t v[kGrp][W];
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (m0 + g < a.nm) ld<VEC>(v[g], row_addr(a.msrc[m0 + g], stripe, off), nb);
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (m0 + g < a.nm) rows_mac1<R, W>(acc, a.tab[m0 + g], v[g]);
+    }
+    for (int x0 = 0; x0 < a.nx; x0 += kGrp) {
+      uint32_t v[kGrp][W];
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (x0 + g < a.nx) ld<VEC>(v[g], row_addr(a.xsrc[x0 + g], stripe, off), nb);
+#pragma unroll
+      for (int g = 0; g < kGrp; ++g)
+        if (x0 + g < a.nx) rows_xor<R, W>(acc, a.xmask[x0 + g], v[g]);
+    }
   } else {
-    // Runtime counts: one row at a time (measured: grouping 8 loads per
-    // wave helped 4 KiB rows by 1-6% but cost 3-4% at 1 MiB;
+    // Runtime counts, large grid: one row at a time (measured: grouping 8
+    // loads per wave helped 4 KiB rows by 1-6% but cost 3-4% at 1 MiB;
     // profiles/r01_bench_configs_grouped.log).
     for (int m = 0; m < a.nm; ++m) {
       uint32_t v[W];
@@ -635,10 +660,6 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     a.rb[a.nr] = m;
     a.rmask[a.nr++] = p.bret[m];
   }
-  // Late-b is the default (measured faster: profiles/r01_bench_multi_staged.log);
-  // XRS_STAGED_LATE=0 selects the all-loads-first kernel.
-  const char* lv = std::getenv("XRS_STAGED_LATE");
-  late = late && !(lv && lv[0] == '0');
   a.nd = p.nd;
   a.na = p.na;
   a.nb = p.nb;
@@ -651,6 +672,14 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, VEC, p.half, blocks);
+  // Late-b wins on grids that fill the chip (bandwidth-bound; measured:
+  // profiles/r01_bench_multi_staged.log).  A grid smaller than one block per
+  // CU is latency-bound: there the all-loads-first kernel pays one memory
+  // round trip instead of two (a per-stripe call on host-mapped staging: one
+  // PCIe round trip).  XRS_STAGED_LATE=0 / =1 forces either kernel.
+  const char* lv = std::getenv("XRS_STAGED_LATE");
+  if (lv && *lv) late = late && lv[0] != '0';
+  else late = late && blocks >= kLatencyGrid;
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   // (A compile-time survivor count, ND = 12, let the scheduler hoist the
   // b-row loads: 225-232 VGPRs plus scratch.  Runtime nd only.)
@@ -750,6 +779,9 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kRows, VEC, p.len, blocks);
+  // XRS_ROWS_GROUPED=0 / =1 forces either runtime-count loop (A/B, tests).
+  const char* gv = std::getenv("XRS_ROWS_GROUPED");
+  a.grouped = (gv && *gv) ? gv[0] != '0' : blocks < kLatencyGrid;
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kBlock), 0, stream, a);

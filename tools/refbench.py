@@ -32,14 +32,14 @@ KB, MB = 1 << 10, 1 << 20
 PEAK = 8.0e12
 # README.md:80-118 (MB/s = 1e6 B/s, one i7-7700HQ core).
 README_MBS = {
-    "(12+4)-4KB": 10895.15, "(12+4)-1MB": 7530.84, "(12+4)-8MB": 6579.53,
-    "(12+4)-4KB-reconst_1_data_vects": 10334.99, "(12+4)-4KB-reconst_2_data_vects": 9654.17,
-    "(12+4)-4KB-reconst_3_data_vects": 8164.76, "(12+4)-4KB-reconst_4_data_vects": 7404.41,
-    "(12+4)-4KB-update": 26312.14,
-    "(12+4)-4KB-replace_1_data_vects": 44082.57, "(12+4)-4KB-replace_2_data_vects": 26554.30,
-    "(12+4)-4KB-replace_3_data_vects": 19583.16, "(12+4)-4KB-replace_4_data_vects": 16636.82,
-    "(12+4)-4KB-replace_5_data_vects": 14301.15, "(12+4)-4KB-replace_6_data_vects": 13121.98,
-    "(12+4)-4KB-replace_7_data_vects": 12028.10, "(12+4)-4KB-replace_8_data_vects": 11300.55,
+    "Encode/(12+4)-4KB": 10895.15, "Encode/(12+4)-1MB": 7530.84, "Encode/(12+4)-8MB": 6579.53,
+    "Reconst/(12+4)-4KB-reconst_1_data_vects": 10334.99, "Reconst/(12+4)-4KB-reconst_2_data_vects": 9654.17,
+    "Reconst/(12+4)-4KB-reconst_3_data_vects": 8164.76, "Reconst/(12+4)-4KB-reconst_4_data_vects": 7404.41,
+    "Update/(12+4)-4KB": 26312.14,
+    "Replace/(12+4)-4KB-replace_1_data_vects": 44082.57, "Replace/(12+4)-4KB-replace_2_data_vects": 26554.30,
+    "Replace/(12+4)-4KB-replace_3_data_vects": 19583.16, "Replace/(12+4)-4KB-replace_4_data_vects": 16636.82,
+    "Replace/(12+4)-4KB-replace_5_data_vects": 14301.15, "Replace/(12+4)-4KB-replace_6_data_vects": 13121.98,
+    "Replace/(12+4)-4KB-replace_7_data_vects": 12028.10, "Replace/(12+4)-4KB-replace_8_data_vects": 11300.55,
 }
 
 
@@ -62,7 +62,7 @@ def timed(fn, reps=10, warm=2):
 
 def emit(bench, name, size, n, secs, bytes_per_stripe):
     total = n * bytes_per_stripe
-    ref = README_MBS.get(name)
+    ref = README_MBS.get(bench.replace("BenchmarkXRS_", "") + "/" + name)
     rate = total / secs
     print(json.dumps({
         "bench": f"{bench}/{name}", "vect_bytes": size, "stripes": n,
@@ -114,14 +114,15 @@ def main():
         else:
             bps = (D + i) * size
         secs = timed(lambda j: x.reconst_batched(t.data_ptr(), size, sh, st, n, has, lost, s))
-        emit("BenchmarkXRS_Reconst", f"(12+4)-4KB-reconst_{i}_data_vects", size, n, secs, bps)
+        emit("BenchmarkXRS_Reconst", f"(12+4)-4KB-reconst_{i}_data_vects", size, n,
+             secs, bps)
     # BenchmarkXRS_Update: vects[row] -> newData, parity vects[d:]
     row = 5
     new = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=dev)
     par = t.data_ptr() + D * sh
     secs = timed(lambda j: x.update_batched(t.data_ptr() + row * sh, st, new.data_ptr(), size,
                                             size, row, par, sh, st, n, s))
-    emit("BenchmarkXRS_Update", "(12+4)-4KB-update", size, n, secs, (2 * P + 2) * size)
+    emit("BenchmarkXRS_Update", "(12+4)-4KB", size, n, secs, (2 * P + 2) * size)
     del new
     # BenchmarkXRS_Replace: data vects[:n] at rows 0..n-1, parity vects[d:]
     for k in range(1, D - P + 1):

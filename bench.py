@@ -108,7 +108,7 @@ def cpu_baseline(seconds: float, step_bytes: dict):
     rn = _cpu_rates(o, seconds / 2, threads)
     return {
         "value": round(mix(r1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-        "simd": "avx2" if lib().oxrs_simd_available() else "scalar",
+        "simd": ("scalar", "avx2", "avx512bw")[lib().oxrs_simd_level()],
         "cpu_model": _cpu_model(),
         "gibps": {k: round(v / 2**30, 3) for k, v in r1.items()},
         "multi_thread": {"threads": threads, "value": round(mix(rn), 3),

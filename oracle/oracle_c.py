@@ -62,6 +62,7 @@ def lib():
         L.oxrs_encode_batch.argtypes = [P, P, Z, Z, ctypes.c_long, I]
         L.oxrs_reconst_one_batch.argtypes = [P, P, Z, Z, ctypes.c_long, I, I]
         L.oxrs_simd_available.restype = I
+        L.oxrs_simd_level.restype = I
         _lib = L
     return _lib
 

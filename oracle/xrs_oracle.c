@@ -20,8 +20,9 @@
  *     Encode(dst, src) = XOR of all src into dst; dst may alias src[0].
  *
  * The CPU baseline (oxrs_*_batch) follows the same design as the reference's
- * dependency: 16-entry low/high-nibble product tables looked up with AVX2
- * vpshufb, and, like xrs.go Encode, a second pass for the piggyback XOR.
+ * dependency: 16-entry low/high-nibble product tables looked up with vpshufb
+ * (AVX-512BW when the CPU has it, else AVX2; the dependency dispatches the same way)
+ * and, like xrs.go Encode, a second pass for the piggyback XOR.
  */
 #include "xrs_oracle.h"
 
@@ -338,7 +339,7 @@ int oxrs_replace(const oxrs *x, uint8_t *const *data, const int *rows, int n,
   return OXRS_OK;
 }
 
-/* ====================================================== CPU baseline (AVX2) */
+/* ============================================ CPU baseline (AVX-512BW / AVX2) */
 typedef struct { uint8_t lo[16], hi[16]; } nib_tab;
 
 static void make_nib(uint8_t c, nib_tab *t) {
@@ -348,14 +349,28 @@ static void make_nib(uint8_t c, nib_tab *t) {
   }
 }
 
-int oxrs_simd_available(void) {
+/* SIMD level of the baseline: 2 = AVX-512BW (64-byte vpshufb), 1 = AVX2,
+ * 0 = scalar.  The reference's dependency picks the widest path the CPU has
+ * (templexxx/cpu feature detection); OXRS_SIMD=avx2 or
+ * =scalar caps it for A/B runs. */
+int oxrs_simd_level(void) {
+  static int hw = -1;
+  if (hw < 0) {
+    int l = 0;
 #if defined(__x86_64__)
-  __builtin_cpu_init();
-  return __builtin_cpu_supports("avx2") ? 1 : 0;
-#else
-  return 0;
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("avx2")) l = 1;
+    if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")) l = 2;
 #endif
+    hw = l;
+  }
+  const char *cap = getenv("OXRS_SIMD");  /* read per call: tests switch it */
+  if (cap && strcmp(cap, "scalar") == 0) return 0;
+  if (cap && strcmp(cap, "avx2") == 0 && hw > 1) return 1;
+  return hw;
 }
+
+int oxrs_simd_available(void) { return oxrs_simd_level() > 0; }
 
 #if defined(__x86_64__)
 /* out[r] (=|^=) sum_j tab[r*nin+j] * in[j], r < nout, over n bytes (n % 32 == 0
@@ -403,6 +418,50 @@ __attribute__((target("avx2"))) static void xor_avx2(uint8_t *dst, const uint8_t
   }
   for (; i < n; i++) dst[i] ^= src[i];
 }
+
+/* The same two loops on 64-byte zmm registers (AVX-512BW vpshufb); the
+ * three-way XOR is one vpternlogq. */
+__attribute__((target("avx512f,avx512bw"))) static void gf_matmul_avx512(
+    const nib_tab *tab, int nout, int nin, const uint8_t *const *in, uint8_t *const *out,
+    size_t n) {
+  const __m512i mask = _mm512_set1_epi8(0x0f);
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    __m512i acc[8];
+    for (int r = 0; r < nout; r++) acc[r] = _mm512_setzero_si512();
+    for (int j = 0; j < nin; j++) {
+      __m512i v = _mm512_loadu_si512((const void *)(in[j] + i));
+      __m512i lo = _mm512_and_si512(v, mask);
+      __m512i hi = _mm512_and_si512(_mm512_srli_epi64(v, 4), mask);
+      for (int r = 0; r < nout; r++) {
+        const nib_tab *t = &tab[r * nin + j];
+        __m512i tl = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i *)t->lo));
+        __m512i th = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i *)t->hi));
+        acc[r] = _mm512_ternarylogic_epi64(acc[r], _mm512_shuffle_epi8(tl, lo),
+                                           _mm512_shuffle_epi8(th, hi), 0x96);
+      }
+    }
+    for (int r = 0; r < nout; r++) _mm512_storeu_si512((void *)(out[r] + i), acc[r]);
+  }
+  if (i < n) {
+    const uint8_t *in2[OXRS_MAX_VECTS];
+    uint8_t *out2[8];
+    for (int j = 0; j < nin; j++) in2[j] = in[j] + i;
+    for (int r = 0; r < nout; r++) out2[r] = out[r] + i;
+    gf_matmul_avx2(tab, nout, nin, in2, out2, n - i);
+  }
+}
+
+__attribute__((target("avx512f,avx512bw"))) static void xor_avx512(uint8_t *dst,
+                                                                    const uint8_t *src, size_t n) {
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    __m512i a = _mm512_loadu_si512((const void *)(dst + i));
+    __m512i b = _mm512_loadu_si512((const void *)(src + i));
+    _mm512_storeu_si512((void *)(dst + i), _mm512_xor_si512(a, b));
+  }
+  xor_avx2(dst + i, src + i, n - i);
+}
 #endif
 
 static void gf_matmul_scalar(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
@@ -421,10 +480,12 @@ static void gf_matmul_scalar(const nib_tab *tab, int nout, int nin, const uint8_
 static void gf_matmul(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
                       uint8_t *const *out, size_t n) {
 #if defined(__x86_64__)
-  if (oxrs_simd_available()) {
+  const int level = oxrs_simd_level();
+  if (level > 0) {
     for (int r0 = 0; r0 < nout; r0 += 8) {
       int nr = nout - r0 < 8 ? nout - r0 : 8;
-      gf_matmul_avx2(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n);
+      if (level > 1) gf_matmul_avx512(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n);
+      else gf_matmul_avx2(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n);
     }
     return;
   }
@@ -434,7 +495,9 @@ static void gf_matmul(const nib_tab *tab, int nout, int nin, const uint8_t *cons
 
 static void xor_fast(uint8_t *dst, const uint8_t *src, size_t n) {
 #if defined(__x86_64__)
-  if (oxrs_simd_available()) { xor_avx2(dst, src, n); return; }
+  const int level = oxrs_simd_level();
+  if (level > 1) { xor_avx512(dst, src, n); return; }
+  if (level > 0) { xor_avx2(dst, src, n); return; }
 #endif
   xor_into(dst, src, n);
 }

@@ -67,10 +67,11 @@ int oxrs_rs_encode(const oxrs *x, uint8_t *const *vects, size_t size);
 int oxrs_rs_reconst(const oxrs *x, uint8_t *const *vects, size_t size,
                     const int *dp_has, int n_has, const int *need, int n_need);
 
-/* ---- CPU baseline (the reference's algorithm: 4-bit split tables, AVX2 vpshufb,
+/* ---- CPU baseline (the reference's algorithm: 4-bit split tables, AVX-512BW or AVX2 vpshufb,
  *      two passes like xrs.go Encode: RS then piggyback XOR) over a contiguous
  *      batch: stripe s, shard i at base + s*stripe_stride + i*size. ---- */
 int oxrs_simd_available(void);
+int oxrs_simd_level(void); /* 2 = AVX-512BW, 1 = AVX2, 0 = scalar */
 int oxrs_encode_batch(const oxrs *x, uint8_t *base, size_t size,
                       size_t stripe_stride, long n_stripes, int threads);
 int oxrs_reconst_one_batch(const oxrs *x, uint8_t *base, size_t size,

@@ -223,3 +223,32 @@ def test_c_vs_numpy_other_configs(rng):
             xc.reconst(a1, has, need)
             xp.reconst(a2, has, need)
             assert all(np.array_equal(a, b) for a, b in zip(a1, a2))
+
+
+# ------------------------------------------------ CPU baseline (batch) paths
+@pytest.mark.parametrize("level", ["scalar", "avx2", "native"])
+@pytest.mark.parametrize("d,p", [(12, 4), (5, 5), (20, 3)])
+def test_cpu_baseline_batch_paths(monkeypatch, level, d, p):
+    """The timed CPU baseline (oxrs_encode_batch / oxrs_reconst_one_batch, at
+    every SIMD level: scalar, AVX2, and the CPU's widest, AVX-512BW here) equals
+    the per-stripe restatement, on ragged sizes and several threads.  The GPU
+    tests use the batch path as their reference, so it is pinned here."""
+    from oracle.oracle_c import lib
+    if level == "avx2" and lib().oxrs_simd_level() < 1:
+        pytest.skip("no AVX2")
+    if level != "native":
+        monkeypatch.setenv("OXRS_SIMD", level)
+    rng = np.random.default_rng(11)
+    o = OracleXRS(d, p)
+    for size, n, threads in ((2, 3, 1), (34, 5, 2), (4096, 7, 3), (40000, 3, 2), (65602, 2, 1)):
+        host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+        ref = host.copy()
+        for s in range(n):
+            v = [ref[s, i] for i in range(d + p)]
+            o.encode(v)
+        o.encode_batch(host, size, n, threads)
+        assert np.array_equal(host, ref), (level, size)
+        k = int(rng.integers(0, d))
+        host[:, k] = 0x5A
+        o.reconst_one_batch(host, size, n, k, threads)
+        assert np.array_equal(host, ref), (level, size, k)

@@ -59,3 +59,47 @@ def test_queue_errors():
     with pytest.raises(xrs_amd.XRSError):
         xrs_amd.XRSQueue(x, 63)
     q.close()
+
+
+@pytest.mark.parametrize("size", [4096, 384 << 10, (4 << 20) + 2])
+def test_sync_calls_from_many_threads(size):
+    """The per-stripe sync API on ONE codec from many threads at once (every
+    staging mode: zero-copy, pinned, direct): every call of every kind is
+    bit-exact to the oracle (the codec is shared, its staging is not racy)."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    n_threads, per_thread = (8, 6) if size <= (1 << 20) else (4, 1)
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(2000 + t))
+        try:
+            for i in range(per_thread):
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+                ref = [a.copy() for a in v]
+                o.encode(ref)
+                x.encode(v)
+                assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, i)
+                lost = [int(j) for j in rng.permutation(D + P)[:3]]
+                has = [j for j in range(D + P) if j not in lost]
+                r1, r2 = [a.copy() for a in v], [a.copy() for a in v]
+                for j in lost:
+                    r1[j][:] = 0
+                    r2[j][:] = 0
+                x.reconst(r1, has, lost)
+                o.reconst(r2, has, lost)
+                assert all(np.array_equal(a, b) for a, b in zip(r1, r2)), ("rec", t, i)
+                row = int(rng.integers(0, D))
+                new = rng.integers(0, 256, size=size, dtype=np.uint8)
+                p1, p2 = [a.copy() for a in v[D:]], [a.copy() for a in v[D:]]
+                x.update(v[row], new, row, p1)
+                o.update(v[row], new, row, p2)
+                assert all(np.array_equal(a, b) for a, b in zip(p1, p2)), ("upd", t, i)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]

@@ -103,7 +103,9 @@ def main():
                     has = list(range(lost, D + P))
                     secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has,
                                                              need, s))
-                    emit(f"reconst_{lost}_{mode}", size, n, secs, n * (D + lost) * size, sh)
+                    # xrs_test.go:565-572: one lost data vect is ReconstOne, 9*S
+                    per = 9 * size if lost == 1 else (D + lost) * size
+                    emit(f"reconst_{lost}_{mode}", size, n, secs, n * per, sh)
             os.environ.pop("XRS_RECONST", None)
             os.environ.pop("XRS_STAGED_LATE", None)
             del t

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Sweep XRS_BLOCK_ORDER over the four headline launches through the product
 launchers (interleaved rounds, median per K).  Prints one JSON line per
-(launch, K); "default" is the library's own choice."""
+(launch, K); "default" is the library's own choice.  CASES=staged sweeps the
+staged general-Reconst kernel instead (2 and 4 lost data vects; GB/s of the
+bytes it moves, side effects included: 16.5*S and 17.5*S per stripe)."""
 import json
 import os
 import sys
@@ -33,7 +35,21 @@ def main():
     x = xrs_amd.XRS(D, P)
     s = torch.cuda.current_stream().cuda_stream
     cases = []
-    for size, n in ((4096, 65536), (1 << 20, 512)):
+    staged = os.environ.get("CASES") == "staged"
+    sizes = ((4096, 65536), (1 << 20, 512))
+    if os.environ.get("CASES") == "staged":
+        sizes = ((4096, 65536), (64 << 10, 4096), (1 << 20, 256), (8 << 20, 32))
+    for size, n in sizes:
+        if staged:
+            shard, stripe = xrs_amd.batch_strides(size, D + P)
+            buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
+            for lost, moved in ((2, 16.5), (4, 17.5)):
+                cases.append((f"reconst_{lost}_{size}", int(moved * size * n), buf,
+                              lambda b=buf.data_ptr(), sz=size, sh=shard, st=stripe, nn=n,
+                              lo=lost: x.reconst_batched(b, sz, sh, st, nn,
+                                                         list(range(lo, D + P)),
+                                                         list(range(lo)), s)))
+            continue
         shard, stripe = xrs_amd.batch_strides(size, D + P)
         buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
         base = buf.data_ptr()

@@ -609,7 +609,10 @@ enum class Shape { kPair, kRows, kStaged };
 //  * rows (ReconstOne): 4 KiB vects want one range per XCD (K = nblk/8),
 //    8-128 KiB vects the plain order, >= 512 KiB vects K = half / 8 KiB up
 //    to 256 (1 MiB: 64, 8 MiB: 256; profiles/r01_order_sweep.log);
-//  * staged (general Reconst) reads both halves of every shard like pair.
+//  * staged (general Reconst): 4 KiB vects one range per XCD (+6-7% over
+//    K = 32), 512 KiB-2 MiB vects K = 128, >= 2 MiB vects the plain order
+//    (8 MiB: K = 256 lost 5-9%), K = 32 between
+//    (profiles/r01_order_sweep_staged.log).
 // The byte-granular (!VEC) path keeps the plain order.  XRS_BLOCK_ORDER=<K>
 // overrides (0: plain order; "full": one range per XCD) for A/B runs.
 BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
@@ -621,8 +624,12 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
     return o;
   }
   switch (shape) {
-    case Shape::kPair:
-    case Shape::kStaged: o.k = 32; break;
+    case Shape::kPair: o.k = 32; break;
+    case Shape::kStaged:
+      if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
+      else if (len < (256u << 10)) o.k = 32;
+      else if (len < (1u << 20)) o.k = 128;
+      break;  // half >= 1 MiB: plain order
     case Shape::kRows:
       if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
       else if (len >= (256u << 10)) o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 13));

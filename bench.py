@@ -139,6 +139,7 @@ def main():
     ap.add_argument("--enc-stripes", type=int, default=65536)
     ap.add_argument("--rec-stripes", type=int, default=512)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--ramp-seconds", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -178,6 +179,14 @@ def main():
     x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
     x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, stream)
     torch.cuda.synchronize()
+    # Clock ramp (setup, untimed): an idle MI355X runs its first ~50 launches
+    # of this size up to 30% slower (tools/first_alloc_probe.py,
+    # profiles/r01_first_alloc.log).  Repeat the (idempotent) setup encode for
+    # --ramp-seconds before the W warmup steps.
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < args.ramp_seconds:
+        x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
+        torch.cuda.synchronize()
     # The four timed launches of a step, in order: (key, kernel, algorithmic
     # bytes per launch, read bytes per launch, launcher).
     launches = [

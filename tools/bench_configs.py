@@ -9,6 +9,7 @@ Update (2p+2)*S, Replace(n) (n+2p)*S per stripe.  One JSON line per case.
 import json
 import os
 import sys
+import time
 
 import torch
 
@@ -20,9 +21,14 @@ D, P = 12, 4
 PEAK = 8.0e12
 
 
-def timed(fn, reps=10, warm=2):
-    for i in range(warm):
+def timed(fn, reps=10, warm=2, ramp=0.3):
+    # An idle GPU runs its first launches slowly (profiles/r01_first_alloc.log):
+    # warm for `ramp` seconds as well as `warm` launches.
+    t0, i = time.perf_counter(), 0
+    while i < warm or time.perf_counter() - t0 < ramp:
         fn(i)
+        torch.cuda.synchronize()
+        i += 1
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()

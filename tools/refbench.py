@@ -20,6 +20,7 @@ tools/sync_bench (`ref` mode).
 import json
 import os
 import sys
+import time
 
 import torch
 
@@ -47,9 +48,14 @@ def size_str(n):  # byteToStr, xrs_test.go:682
     return f"{n // MB}MB" if n >= MB else f"{n // KB}KB"
 
 
-def timed(fn, reps=10, warm=2):
-    for i in range(warm):
+def timed(fn, reps=10, warm=2, ramp=0.3):
+    # An idle GPU runs its first launches slowly (profiles/r01_first_alloc.log):
+    # warm for `ramp` seconds as well as `warm` launches.
+    t0, i = time.perf_counter(), 0
+    while i < warm or time.perf_counter() - t0 < ramp:
         fn(i)
+        torch.cuda.synchronize()
+        i += 1
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()

@@ -1,0 +1,102 @@
+"""Randomised parity of the batched device API against the oracle.
+
+Each case draws a codec (d, p), a vect size (even, 2 B to 40 KiB), a stripe
+count, a layout (shard and stripe strides with random padding, and a base
+offset 0..15 so both the 16-byte and the byte-granular kernels run) and one
+operation (Encode, ReconstOne, Reconst with random losses and needs, Update,
+Replace).  The GPU buffer after the call must equal the oracle applied stripe
+by stripe to a host copy, byte for byte, including every byte outside the
+shards (nothing else may be written).  Seeded; bounded to a few seconds."""
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+CODECS = [(12, 4), (10, 4), (6, 3), (4, 2), (5, 5), (20, 4), (1, 2), (30, 6), (3, 9), (16, 8)]
+OPS = ["encode", "reconst_one", "reconst", "update", "replace"]
+
+
+def draw_case(rng):
+    d, p = CODECS[int(rng.integers(0, len(CODECS)))]
+    size = int(rng.choice([2, 34, 1024, 1026, 4096, 4112, 6000, 40960]))
+    n = int(rng.integers(1, 40))
+    shard = size + int(rng.choice([0, 0, 2, 16, 256]))
+    stripe = (d + p) * shard + int(rng.choice([0, 0, 6, 64]))
+    base = int(rng.choice([0, 0, 0, 1, 8]))
+    return d, p, size, n, shard, stripe, base, OPS[int(rng.integers(0, len(OPS)))]
+
+
+def vects_of(buf, base, s, shard, stripe, size, count, first=0):
+    o = base + s * stripe
+    return [buf[o + (first + i) * shard: o + (first + i) * shard + size] for i in range(count)]
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_batched_fuzz_vs_oracle(seed):
+    rng = np.random.Generator(np.random.PCG64(9000 + seed))
+    dev = torch.device("cuda:0")
+    s_ = torch.cuda.current_stream().cuda_stream
+    for case in range(30):
+        d, p, size, n, shard, stripe, base, op = draw_case(rng)
+        x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+        total = base + n * stripe + 64
+        host = rng.integers(0, 256, size=total, dtype=np.uint8)
+        # start from encoded stripes (reconstruction needs consistent parity)
+        for s in range(n):
+            o.encode(vects_of(host, base, s, shard, stripe, size, d + p))
+        ref = host.copy()
+        t = torch.from_numpy(host).to(dev)
+        ptr = t.data_ptr() + base
+        tag = (seed, case, d, p, size, n, shard, stripe, base, op)
+        if op == "encode":
+            for s in range(n):  # garbage parity in, must be overwritten
+                for v in vects_of(host, base, s, shard, stripe, size, p, first=d):
+                    v[:] = rng.integers(0, 256, size=size, dtype=np.uint8)
+            t.copy_(torch.from_numpy(host))
+            x.encode_batched(ptr, size, shard, stripe, n, s_)
+        elif op == "reconst_one":
+            k = int(rng.integers(0, d))
+            for s in range(n):
+                vects_of(host, base, s, shard, stripe, size, 1, first=k)[0][:] = 0x5A
+            t.copy_(torch.from_numpy(host))
+            x.reconst_one_batched(ptr, size, shard, stripe, n, k, s_)
+        elif op == "reconst":
+            lost = [int(v) for v in rng.permutation(d + p)[: int(rng.integers(0, p + 1))]]
+            need = lost[: int(rng.integers(0, len(lost) + 1))]
+            has = [i for i in range(d + p) if i not in lost]
+            for s in range(n):
+                for i in lost:
+                    vects_of(host, base, s, shard, stripe, size, 1, first=i)[0][:] = 0xA5
+            ref = host.copy()
+            t.copy_(torch.from_numpy(host))
+            x.reconst_batched(ptr, size, shard, stripe, n, has, need, s_)
+            for s in range(n):
+                o.reconst(vects_of(ref, base, s, shard, stripe, size, d + p), has, need)
+        elif op == "update":
+            row = int(rng.integers(0, d))
+            new = rng.integers(0, 256, size=n * size, dtype=np.uint8)
+            tn = torch.from_numpy(new).to(dev)
+            old_ptr = ptr + row * shard
+            x.update_batched(old_ptr, stripe, tn.data_ptr(), size, size, row, ptr + d * shard,
+                             shard, stripe, n, s_)
+            for s in range(n):
+                old = vects_of(ref, base, s, shard, stripe, size, 1, first=row)[0]
+                o.update(old, new[s * size:(s + 1) * size],
+                         row, vects_of(ref, base, s, shard, stripe, size, p, first=d))
+        else:  # replace
+            k = int(rng.integers(1, d + 1))
+            rows = [int(v) for v in rng.permutation(d)[:k]]
+            x.replace_batched(ptr, shard, stripe, rows, size, ptr + d * shard, shard, stripe, n,
+                              s_)
+            for s in range(n):  # data[i] (for row rows[i]) is vect i of the stripe
+                o.replace(vects_of(ref, base, s, shard, stripe, size, k), rows,
+                          vects_of(ref, base, s, shard, stripe, size, p, first=d))
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad = np.nonzero(got != ref)[0]
+            raise AssertionError(f"{tag}: {len(bad)} bytes differ, first at {bad[0]}")

@@ -103,3 +103,46 @@ def test_sync_calls_from_many_threads(size):
     for t in th:
         t.join()
     assert not errors, errors[:3]
+
+
+def test_queue_close_while_callers_in_flight():
+    """close() while 16 threads keep submitting: every call either returns a
+    bit-exact result or raises (the queue is closed); none hangs, and the
+    queue is torn down only after the last call has left."""
+    size = 4096
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=64, max_wait_us=200)
+    ok, closed, bad = [0], [0], []
+    lock = threading.Lock()
+    go = threading.Event()
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(3000 + t))
+        go.wait()
+        for i in range(1 << 30):  # until the queue is closed
+            v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+            ref = [a.copy() for a in v]
+            o.encode(ref)
+            try:
+                q.encode(v)
+            except xrs_amd.XRSError:
+                with lock:
+                    closed[0] += 1
+                return
+            if not all(np.array_equal(a, b) for a, b in zip(v, ref)):
+                bad.append((t, i))
+            with lock:
+                ok[0] += 1
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    go.set()
+    import time
+    time.sleep(0.3)
+    q.close()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th), "a caller hung after close()"
+    assert not bad, bad[:3]
+    assert ok[0] > 0 and closed[0] > 0, (ok[0], closed[0])

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 __all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
 
@@ -23,6 +24,7 @@ LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
 
 XRS_ERR_SIZE_NOT_EVEN = -2
 XRS_ERR_ILLEGAL_DATA_INDEX = -3
+XRS_ERR_INVALID_ARG = -9
 
 
 class XRSError(Exception):
@@ -359,6 +361,8 @@ class XRSQueue:
     def __init__(self, codec: XRS, size: int, max_batch_stripes: int = 1024,
                  max_wait_us: int = 50):
         self._h = None
+        self._cv = threading.Condition()
+        self._inflight = 0
         h = ctypes.c_void_p()
         _raise(_lib.xrs_queue_new(codec.handle, size, max_batch_stripes, max_wait_us,
                                   ctypes.byref(h)), size)
@@ -368,19 +372,35 @@ class XRSQueue:
         self.batch_stripes = _lib.xrs_queue_batch_stripes(h)
 
     def close(self, _free=_lib.xrs_queue_free):
-        if self._h is not None and self._h.value:
-            _free(self._h)
-            self._h = None
+        """New calls fail from here on; calls in flight complete first."""
+        with self._cv:
+            h, self._h = self._h, None
+            self._cv.wait_for(lambda: self._inflight == 0)
+        if h is not None and h.value:
+            _free(h)
 
     def __del__(self):
         self.close()
 
+    def _call(self, fn, *args):
+        with self._cv:
+            h = self._h
+            if h is None:
+                return XRS_ERR_INVALID_ARG
+            self._inflight += 1
+        try:
+            return fn(h, *args)
+        finally:
+            with self._cv:
+                self._inflight -= 1
+                self._cv.notify_all()
+
     def encode(self, vects) -> None:
-        _raise(_lib.xrs_queue_encode(self._h, _ptrs(vects), len(vects)), self.size)
+        _raise(self._call(_lib.xrs_queue_encode, _ptrs(vects), len(vects)), self.size)
 
     def reconst_one(self, vects, need_reconst: int) -> None:
-        _raise(_lib.xrs_queue_reconst_one(self._h, _ptrs(vects), len(vects), int(need_reconst)),
-               need_reconst)
+        _raise(self._call(_lib.xrs_queue_reconst_one, _ptrs(vects), len(vects),
+                          int(need_reconst)), need_reconst)
 
     def stats(self) -> dict:
         """Batches and stripes run so far, and summed device / queueing ns."""

@@ -8,9 +8,10 @@
 //   caller thread: reserve a slot in the open batch -> copy its vects into the
 //     batch's pinned staging (callers copy in parallel) -> wait -> copy its
 //     outputs back -> release the slot.
-//   worker threads (XRS_QUEUE_WORKERS, default 2): run a batch when it is full, or when it has waited
-//     max_wait_us with every reserved slot filled: one H2D of the whole batch,
-//     one kernel over all its stripes, one D2H, on the batch's own stream.
+//   worker threads (XRS_QUEUE_WORKERS, default 2): run a batch when it is
+//     full, or when it has waited max_wait_us with every reserved slot
+//     filled: one H2D of the whole batch, one kernel over all its stripes,
+//     one D2H, on the batch's own stream.
 //     Batches of up to XRS_QUEUE_ZC_MAX bytes (default 4 MiB) skip both
 //     copies: the kernel reads and writes the pinned, device-mapped staging
 //     over PCIe (measured faster than DMA at these sizes).
@@ -75,6 +76,7 @@ struct xrs_queue {
   Batch b[kBatches];
   int open = -1;
   int running = 0;  // batches being run by workers
+  int active = 0;   // callers inside submit() (xrs_queue_free waits for 0)
   bool stop = false;
   // statistics (guarded by mu): batches run, stripes run, device time
   // (launch to stream sync) and queueing time (open to launch) summed over
@@ -124,11 +126,13 @@ void xrs_queue::run(int i) {
 void xrs_queue::work() {
   if (device >= 0) (void)hipSetDevice(device);
   std::unique_lock<std::mutex> lk(mu);
-  while (!stop) {
+  for (;;) {
     int pick = -1;
+    bool pending = false;  // a batch some caller still waits on
     Clock::time_point next = Clock::now() + max_wait;
     for (int i = 0; i < n_batches && pick < 0; ++i) {
       Batch& bt = b[i];
+      if (bt.state == OPEN || bt.state == CLOSED) pending = true;
       if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
       if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
         // A small batch runs at once when no batch is in flight (a lone
@@ -137,7 +141,8 @@ void xrs_queue::work() {
         // grows until max_wait has passed.
         const auto due = bt.opened + max_wait;
         const bool small = bt.reserved * stripe_bytes <= zc_max;
-        if ((running == 0 && small) || Clock::now() >= due) {
+        // (stopping: drain, every caller already in gets its result)
+        if ((running == 0 && small) || stop || Clock::now() >= due) {
           bt.state = CLOSED;
           if (open == i) open = -1;
           pick = i;
@@ -147,6 +152,7 @@ void xrs_queue::work() {
       }
     }
     if (pick < 0) {
+      if (stop && !pending) break;
       cv_work.wait_until(lk, next);
       continue;
     }
@@ -198,8 +204,13 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
   uint64_t gen;
   {
     std::unique_lock<std::mutex> lk(mu);
+    ++active;
     for (;;) {
-      if (stop) return XRS_ERR_INVALID_ARG;
+      if (stop) {
+        --active;
+        cv_free.notify_all();
+        return XRS_ERR_INVALID_ARG;
+      }
       if (open >= 0 && b[open].key == key && b[open].reserved < max_batch) break;
       if (open >= 0) {  // different op or full: close it, the worker runs it
         b[open].state = CLOSED;
@@ -256,8 +267,9 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
     if (++bt.released == bt.reserved) {
       bt.state = FREE;
       bt.gen++;
-      cv_free.notify_all();
     }
+    --active;
+    cv_free.notify_all();
   }
   return err;
 }
@@ -313,9 +325,14 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
 void xrs_queue_free(xrs_queue* q) {
   if (!q) return;
   {
-    std::lock_guard<std::mutex> lk(q->mu);
+    // New calls fail from here on; calls already holding a slot complete
+    // (the workers drain every open batch before they exit), and the queue
+    // is torn down only after the last caller has left submit().
+    std::unique_lock<std::mutex> lk(q->mu);
     q->stop = true;
     q->cv_work.notify_all();
+    q->cv_free.notify_all();
+    q->cv_free.wait(lk, [q] { return q->active == 0; });
   }
   for (auto& w : q->worker)
     if (w.joinable()) w.join();

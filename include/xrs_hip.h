@@ -116,6 +116,15 @@ int xrs_update_batched(const xrs_codec *codec, const uint8_t *old_base, size_t o
                        const uint8_t *new_base, size_t new_stripe_stride, size_t size, int row,
                        uint8_t *parity_base, size_t parity_shard_stride,
                        size_t parity_stripe_stride, size_t n_stripes, void *stream);
+/* Update with one data row per stripe -- a batch of small writes to different
+ * data shards: stripe s applies Update(old_s, new_s, rows[s], parity_s).
+ * rows: n_stripes int32 in device-readable memory (device or host-mapped);
+ * a stripe whose row is not in [0, d) is left untouched. */
+int xrs_update_rows_batched(const xrs_codec *codec, const uint8_t *old_base,
+                            size_t old_stripe_stride, const uint8_t *new_base,
+                            size_t new_stripe_stride, size_t size, const int32_t *rows,
+                            uint8_t *parity_base, size_t parity_shard_stride,
+                            size_t parity_stripe_stride, size_t n_stripes, void *stream);
 /* Replace(data, rows, parity) for every stripe: data i of stripe s at
  * data_base + s*data_stripe_stride + i*data_shard_stride. */
 int xrs_replace_batched(const xrs_codec *codec, const uint8_t *data_base,
@@ -181,18 +190,24 @@ int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling
- * x.Encode / x.ReconstOne) into device batches of up to max_batch_stripes
- * (capped at 64 MiB of staging) with one H2D, one kernel and one D2H per
- * batch.  A batch runs when full, or max_wait_us after it opened once every
- * reserved stripe is staged.  Each call blocks until its own stripe is done
- * and has the semantics of xrs_encode / xrs_reconst_one for vects of the
- * queue's `size`.  Thread-safe; one queue per (codec, vect size). */
+ * x.Encode / x.ReconstOne / x.Update) into device batches of up to
+ * max_batch_stripes (capped at 64 MiB of staging) with one H2D, one kernel
+ * and one D2H per batch; a batch holds calls of one kind (Encode, ReconstOne
+ * of one k, or Update of any rows).  A batch runs when full, or max_wait_us after
+ * it opened once every reserved stripe is staged (at once when small and the
+ * GPU is idle).  Each call blocks until its own stripe is done and has the
+ * semantics of xrs_encode / xrs_reconst_one / xrs_update for vects of the
+ * queue's `size`.  Thread-safe; one queue per (codec, vect size).
+ * xrs_queue_free: later calls fail; calls in flight complete first. */
 typedef struct xrs_queue xrs_queue;
 int xrs_queue_new(const xrs_codec *codec, size_t size, size_t max_batch_stripes, int max_wait_us,
                   xrs_queue **out);
 void xrs_queue_free(xrs_queue *q);
 int xrs_queue_encode(xrs_queue *q, uint8_t *const *vects, int n);
 int xrs_queue_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k);
+/* xrs.go:324 Update(oldData, newData, row, parity), coalesced. */
+int xrs_queue_update(xrs_queue *q, const uint8_t *old_data, const uint8_t *new_data, int row,
+                     uint8_t *const *parity, int n_parity);
 size_t xrs_queue_batch_stripes(const xrs_queue *q);
 /* Counters since xrs_queue_new: out[0] batches run, out[1] stripes run,
  * out[2] ns from each batch's launch to its completion, out[3] ns each batch

@@ -154,3 +154,42 @@ def test_sync_fuzz_vs_oracle(seed):
             x.replace(data, rows, a[d:])
             o.replace(data, rows, b[d:])
         assert all(np.array_equal(s, t) for s, t in zip(a, b)), tag
+
+
+@pytest.mark.parametrize("d,p,size", [(12, 4, 4096), (12, 4, 1026), (12, 4, 34), (30, 6, 4096),
+                                      (1, 2, 4096), (10, 4, 1 << 20), (3, 9, 2)])
+def test_update_rows_batched_vs_oracle(d, p, size):
+    """xrs_update_rows_batched: every stripe its own data row (rows beyond one
+    launch's 24-row chunk and parity beyond one 4-output group included);
+    stripes whose row is not a data row (-1, d) are left untouched."""
+    rng = np.random.Generator(np.random.PCG64(7000 + d * 31 + p + size))
+    dev = torch.device("cuda:0")
+    s_ = torch.cuda.current_stream().cuda_stream
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    n = 200 if size < (1 << 20) else 6
+    stripe = (d + p) * size
+    host = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+    for s in range(n):
+        o.encode(vects_of(host, 0, s, size, stripe, size, d + p))
+    new = rng.integers(0, 256, size=n * size, dtype=np.uint8)
+    rows = rng.integers(0, d, size=n).astype(np.int32)
+    rows[::17] = -1
+    rows[5::23] = d
+    ref = host.copy()
+    for s in range(n):
+        if 0 <= rows[s] < d:
+            o.update(vects_of(ref, 0, s, size, stripe, size, 1, first=int(rows[s]))[0],
+                     new[s * size:(s + 1) * size], int(rows[s]),
+                     vects_of(ref, 0, s, size, stripe, size, p, first=d))
+    # old data row of stripe s: its own row (a clamped row for skipped stripes)
+    olds = np.stack([vects_of(host, 0, s, size, stripe, size, 1,
+                              first=int(min(max(rows[s], 0), d - 1)))[0] for s in range(n)])
+    t = torch.from_numpy(host).to(dev)
+    to = torch.from_numpy(olds.reshape(-1)).to(dev)
+    tn = torch.from_numpy(new).to(dev)
+    tr = torch.from_numpy(rows).to(dev)
+    x.update_rows_batched(to.data_ptr(), size, tn.data_ptr(), size, size, tr.data_ptr(),
+                          t.data_ptr() + d * size, size, stripe, n, s_)
+    torch.cuda.synchronize()
+    got = t.cpu().numpy()
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:5]

@@ -146,3 +146,49 @@ def test_queue_close_while_callers_in_flight():
     assert not any(t.is_alive() for t in th), "a caller hung after close()"
     assert not bad, bad[:3]
     assert ok[0] > 0 and closed[0] > 0, (ok[0], closed[0])
+
+
+@pytest.mark.parametrize("size,d,p", [(4096, 12, 4), (1030, 12, 4), (4096, 1, 2), (65536, 6, 3)])
+def test_queue_concurrent_update(size, d, p):
+    """xrs_queue_update from many threads (rows differ: one batch carries
+    every row, update_rows kernel) interleaved with Encode and ReconstOne on
+    the same queue: parity bit-exact to the oracle after every call."""
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=32, max_wait_us=100)
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(4000 + t))
+        try:
+            v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d + p)]
+            q.encode(v)
+            ref = [a.copy() for a in v]
+            o.encode(ref)
+            assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t)
+            for i in range(12):
+                row = int(rng.integers(0, d))
+                new = rng.integers(0, 256, size=size, dtype=np.uint8)
+                q.update(v[row], new, row, v[d:])
+                o.update(ref[row], new, row, ref[d:])
+                v[row][:] = new
+                ref[row][:] = new
+                assert all(np.array_equal(a, b) for a, b in zip(v[d:], ref[d:])), ("upd", t, i)
+                if i % 4 == 3:
+                    k = int(rng.integers(0, d))
+                    w = [a.copy() for a in v]
+                    w[k][:] = 0
+                    q.reconst_one(w, k)
+                    assert np.array_equal(w[k], v[k]), ("rec", t, i)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    q.close()
+    assert not errors, errors[:3]
+    with pytest.raises(xrs_amd.XRSError, match="illegal data index"):
+        xrs_amd.XRSQueue(x, size).update(np.zeros(size, np.uint8), np.zeros(size, np.uint8), d,
+                                         [np.zeros(size, np.uint8) for _ in range(p)])

@@ -87,6 +87,21 @@ def main():
                                                      n, s))
             emit(f"replace_{nrep}", size, n, secs, n * (nrep + 2 * P) * size, sh)
         del t, new
+    if "rows" in cases:  # Update with a per-stripe random row (xrs_update_rows_batched)
+        for size, n in ((4096, 65536), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 6)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            new = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=dev)
+            old = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=dev)
+            rows = torch.randint(0, D, (n,), dtype=torch.int32, device=dev)
+            par = t.data_ptr() + D * sh
+            secs = timed(lambda i: x.update_rows_batched(old.data_ptr(), size, new.data_ptr(), size,
+                                                         size, rows.data_ptr(), par, sh, st, n, s))
+            emit("update_rows", size, n, secs, n * (2 * P + 2) * size, sh)
+            secs = timed(lambda i: x.update_batched(old.data_ptr(), size, new.data_ptr(), size,
+                                                    size, 5, par, sh, st, n, s))
+            emit("update_one_row", size, n, secs, n * (2 * P + 2) * size, sh)
+            del t, new, old, rows
     if "c5" in cases:  # 1 MiB, 8192 stripes per GPU (the 64k-stripe / 8-GPU split)
         size, n = 1 << 20, 8192
         t, sh, st = batch(size, n, dev, 4)

@@ -123,6 +123,7 @@ int main(int argc, char** argv) {
     std::_Exit(0);
   }
   // --- batching queue, T threads
+  for (int upd = 0; upd < 2; ++upd)
   for (int threads : {1, 8, 32, 128}) {
     xrs_queue* q = nullptr;
     if (xrs_queue_new(c, size, 1024, 50, &q)) return 4;
@@ -136,7 +137,9 @@ int main(int argc, char** argv) {
         for (auto& x : v) p.push_back(x.data());
         long n = 0;
         while (!stop.load(std::memory_order_relaxed)) {
-          if (xrs_queue_encode(q, p.data(), 16)) std::abort();
+          const int rc = upd ? xrs_queue_update(q, p[t % 12], p[(t + 1) % 12], t % 12, p.data() + 12, 4)
+                             : xrs_queue_encode(q, p.data(), 16);
+          if (rc) std::abort();
           ++n;
         }
         total += n;
@@ -149,11 +152,11 @@ int main(int argc, char** argv) {
     uint64_t st[4] = {0, 0, 0, 0};
     xrs_queue_stats(q, st);
     const double nb = st[0] ? static_cast<double>(st[0]) : 1.0;
-    std::printf("{\"api\": \"xrs_queue_encode\", \"vect_bytes\": %zu, \"threads\": %d, "
+    std::printf("{\"api\": \"%s\", \"vect_bytes\": %zu, \"threads\": %d, "
                 "\"stripes_per_s\": %.0f, \"gibps\": %.3f, \"batches\": %llu, "
                 "\"stripes_per_batch\": %.1f, \"run_us_per_batch\": %.1f, "
-                "\"wait_us_per_batch\": %.1f}\n", size, threads, total / dt,
-                total * 16.0 * size / dt / (1 << 30), (unsigned long long)st[0], st[1] / nb,
+                "\"wait_us_per_batch\": %.1f}\n", upd ? "xrs_queue_update" : "xrs_queue_encode",
+                size, threads, total / dt, total * (upd ? 10.0 : 16.0) * size / dt / (1 << 30), (unsigned long long)st[0], st[1] / nb,
                 st[2] / nb / 1e3, st[3] / nb / 1e3);
     std::fflush(stdout);
     xrs_queue_free(q);

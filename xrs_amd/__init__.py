@@ -86,6 +86,7 @@ def _load():
         "xrs_reconst_one_batched": ([P, P, Z, Z, Z, Z, I, P], I),
         "xrs_reconst_batched": ([P, P, Z, Z, Z, Z, IP, I, IP, I, P], I),
         "xrs_update_batched": ([P, P, Z, P, Z, Z, I, P, Z, Z, Z, P], I),
+        "xrs_update_rows_batched": ([P, P, Z, P, Z, Z, P, P, Z, Z, Z, P], I),
         "xrs_replace_batched": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z, P], I),
         "xrs_encode_host": ([P, P, Z, Z, Z, Z], I),
         "xrs_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
@@ -102,6 +103,7 @@ def _load():
         "xrs_queue_free": ([P], None),
         "xrs_queue_encode": ([P, PP, I], I),
         "xrs_queue_reconst_one": ([P, PP, I, I], I),
+        "xrs_queue_update": ([P, P, P, I, PP, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
         "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
@@ -308,6 +310,17 @@ class XRS:
                                      parity_shard_stride, parity_stripe_stride, n_stripes, stream)
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
 
+    def update_rows_batched(self, old_base: int, old_stripe_stride: int, new_base: int,
+                            new_stripe_stride: int, size: int, rows_base: int, parity_base: int,
+                            parity_shard_stride: int, parity_stripe_stride: int, n_stripes: int,
+                            stream: int = 0) -> None:
+        """Update with one data row per stripe; rows_base: device-readable
+        address of n_stripes int32 rows (rows outside [0, d) are skipped)."""
+        _raise(_lib.xrs_update_rows_batched(self._h, old_base, old_stripe_stride, new_base,
+                                            new_stripe_stride, size, rows_base, parity_base,
+                                            parity_shard_stride, parity_stripe_stride, n_stripes,
+                                            stream), size)
+
     def replace_batched(self, data_base: int, data_shard_stride: int, data_stripe_stride: int,
                         replace_rows, size: int, parity_base: int, parity_shard_stride: int,
                         parity_stripe_stride: int, n_stripes: int, stream: int = 0) -> None:
@@ -401,6 +414,10 @@ class XRSQueue:
     def reconst_one(self, vects, need_reconst: int) -> None:
         _raise(self._call(_lib.xrs_queue_reconst_one, _ptrs(vects), len(vects),
                           int(need_reconst)), need_reconst)
+
+    def update(self, old_data, new_data, row: int, parity) -> None:
+        _raise(self._call(_lib.xrs_queue_update, _ptr(old_data), _ptr(new_data), int(row),
+                          _ptrs(parity), len(parity)), row)
 
     def stats(self) -> dict:
         """Batches and stripes run so far, and summed device / queueing ns."""

@@ -468,22 +468,53 @@ int reconst_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stri
   return XRS_OK;
 }
 
+int update_rows_impl(const xrs_codec* x, RowRef old_row, RowRef new_row, size_t size,
+                     const int32_t* rows, int row, const Layout& P, size_t n_stripes,
+                     hipStream_t s);
+
+// xrs.go:324-346 Update.  Delta = old ^ new is linear: parity ^= gen[:, row] *
+// delta (reedsolomon Update [dep], xrs.go:331) and the piggyback XOR of the
+// delta's a-half (:340-344); the update_rows kernel forms the delta first, so
+// it does one GF pass (the pair kernel with old and new as two sources would
+// do two: measured 3% slower at 4 KiB, profiles/r01_bench_configs_rows.log).
 int update_impl(const xrs_codec* x, RowRef old_row, RowRef new_row, size_t size, int row,
                 const Layout& P, size_t n_stripes, hipStream_t s) {
+  return update_rows_impl(x, old_row, new_row, size, nullptr, row, P, n_stripes, s);
+}
+
+// Update with a per-stripe data row (rows: device-readable int32 per stripe),
+// or with one `row` for every stripe (rows == nullptr).  Per-stripe rows are
+// covered in chunks of kMaxSrc per launch (the kernel skips stripes whose row
+// is outside its chunk), outputs in groups of kMaxOut.
+int update_rows_impl(const xrs_codec* x, RowRef old_row, RowRef new_row, size_t size,
+                     const int32_t* rows, int row, const Layout& P, size_t n_stripes,
+                     hipStream_t s) {
   const int d = x->d, p = x->p;
-  std::vector<RowRef> dst;
-  for (int r = 0; r < p; ++r) dst.push_back(P.row(r, 0));
-  // Delta = old ^ new is linear: both rows carry the same column of gen
-  // (reedsolomon Update [dep], xrs.go:331) and the same piggyback (:340-344).
-  std::vector<MulSrc> src(2);
-  src[0].row = old_row;
-  src[1].row = new_row;
-  for (auto& sr : src) {
-    sr.coef.resize(p);
-    for (int r = 0; r < p; ++r) sr.coef[r] = x->g(d + r, row);
-    sr.pb = x->bi_of[row] - d;
+  if (size < 2 || n_stripes == 0) return XRS_OK;
+  const GF& gf = GF::get();
+  xrs::UpdRowsPlan plan;
+  const int first = rows ? 0 : row, last = rows ? d : row + 1;
+  for (int g0 = 0; g0 < p; g0 += xrs::kMaxOut) {
+    for (int j0 = first; j0 < last; j0 += xrs::kMaxSrc) {
+      std::memset(&plan, 0, sizeof(plan));
+      plan.P = std::min(xrs::kMaxOut, p - g0);
+      plan.row0 = j0;
+      plan.nrows = std::min(xrs::kMaxSrc, last - j0);
+      for (int j = 0; j < plan.nrows; ++j) {
+        for (int q = 0; q < plan.P; ++q) plan.tab[j][q] = gf.tab(x->g(d + g0 + q, j0 + j));
+        const int t = x->bi_of[j0 + j] - d - g0;  // xrs.go:340-344 piggyback target
+        plan.pbq[j] = (t >= 0 && t < plan.P) ? static_cast<int8_t>(t) : -1;
+      }
+      plan.old_row = old_row;
+      plan.new_row = new_row;
+      for (int q = 0; q < plan.P; ++q) plan.dst[q] = P.row(g0 + q, 0);
+      plan.rows = reinterpret_cast<uint64_t>(rows);
+      plan.half = size / 2;
+      plan.n_stripes = n_stripes;
+      if (xrs::launch_update_rows(plan, s) != 0) return XRS_ERR_HIP;
+    }
   }
-  return run_pair(dst, src, true, false, size / 2, n_stripes, s);
+  return XRS_OK;
 }
 
 int replace_impl(const xrs_codec* x, const Layout& D, const int* rows, int n, size_t size,
@@ -957,6 +988,24 @@ int xrs_update_batched(const xrs_codec* x, const uint8_t* old_base, size_t old_s
   const RowRef nw{reinterpret_cast<uint64_t>(new_base), new_stripe_stride};
   return update_impl(x, o, nw, size, row, {parity_base, parity_shard_stride, parity_stripe_stride},
                      n_stripes, static_cast<hipStream_t>(stream));
+}
+
+int xrs_update_rows_batched(const xrs_codec* x, const uint8_t* old_base,
+                            size_t old_stripe_stride, const uint8_t* new_base,
+                            size_t new_stripe_stride, size_t size, const int32_t* rows,
+                            uint8_t* parity_base, size_t parity_shard_stride,
+                            size_t parity_stripe_stride, size_t n_stripes, void* stream) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!old_base || !new_base || !parity_base || !rows) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const RowRef o{reinterpret_cast<uint64_t>(old_base), old_stripe_stride};
+  const RowRef nw{reinterpret_cast<uint64_t>(new_base), new_stripe_stride};
+  return update_rows_impl(x, o, nw, size, rows, 0,
+                          {parity_base, parity_shard_stride, parity_stripe_stride}, n_stripes,
+                          static_cast<hipStream_t>(stream));
 }
 
 int xrs_replace_batched(const xrs_codec* x, const uint8_t* data_base, size_t data_shard_stride,

@@ -598,6 +598,66 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   }
 }
 
+// ============================================================ update_rows kernel
+// Update with a per-stripe data row (xrs_plan.h UpdRowsPlan).  The row's
+// coefficient tables are read from the kernel arguments with a per-lane index
+// (lanes of one wave may serve different stripes when H < 1 KiB).
+template <int P, bool VEC>
+struct UpdRowsArgs {
+  GfTab tab[kMaxSrc][P];
+  int32_t pbq[kMaxSrc];
+  RowRef old_row, new_row;
+  RowRef dst[P];
+  const int32_t* rows;
+  int row0, nrows;
+  BlockOrder order;
+  uint64_t half, chunks, total;
+};
+
+template <int P, bool VEC>
+__global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P, VEC> a) {
+  constexpr int W = VEC ? 4 : 1;
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
+  // rows == nullptr: one row for the whole batch (plain Update), table 0.
+  const int r = a.rows ? a.rows[stripe] - a.row0 : 0;
+  if (r < 0 || r >= a.nrows) return;  // another launch's row, or not a data row
+
+  uint32_t oa[W], ob[W], na[W], nw[W], pa[P][W], pb[P][W];
+  const uint64_t o = row_addr(a.old_row, stripe, off), n = row_addr(a.new_row, stripe, off);
+  ld<VEC>(oa, o, nb);
+  ld<VEC>(ob, o + a.half, nb);
+  ld<VEC>(na, n, nb);
+  ld<VEC>(nw, n + a.half, nb);
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    const uint64_t dq = row_addr(a.dst[q], stripe, off);
+    ld<VEC>(pa[q], dq, nb);
+    ld<VEC>(pb[q], dq + a.half, nb);
+  }
+  const int pbq = a.pbq[r];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const uint32_t da = oa[w] ^ na[w], db = ob[w] ^ nw[w];
+    const Sel sa = sel_of(da), sb = sel_of(db);
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const GfTab t = a.tab[r][q];
+      pa[q][w] ^= gmul(t, sa);
+      pb[q][w] = xor_masked(pb[q][w] ^ gmul(t, sb), da, pbq == q ? ~0u : 0u);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    const uint64_t dq = row_addr(a.dst[q], stripe, off);
+    st<VEC>(pa[q], dq, nb);
+    st<VEC>(pb[q], dq + a.half, nb);
+  }
+}
+
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
@@ -714,6 +774,44 @@ int launch_staged_r(const StagedPlan& p, hipStream_t s) {
     }
   }
   return launch_staged_t<4, 4, VEC>(p, s);
+}
+
+template <int P, bool VEC>
+int launch_update_rows_t(const UpdRowsPlan& p, hipStream_t stream) {
+  UpdRowsArgs<P, VEC> a;
+  std::memset(&a, 0, sizeof(a));
+  for (int j = 0; j < p.nrows; ++j) {
+    for (int q = 0; q < P; ++q) a.tab[j][q] = p.tab[j][q];
+    a.pbq[j] = p.pbq[j];
+  }
+  a.old_row = p.old_row;
+  a.new_row = p.new_row;
+  for (int q = 0; q < P; ++q) a.dst[q] = p.dst[q];
+  a.rows = reinterpret_cast<const int32_t*>(p.rows);
+  a.row0 = p.row0;
+  a.nrows = p.nrows;
+  a.half = p.half;
+  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.total = a.chunks * p.n_stripes;
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kPair, VEC, p.half, blocks);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  hipLaunchKernelGGL((update_rows_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <bool VEC>
+int launch_update_rows_p(const UpdRowsPlan& p, hipStream_t s) {
+  switch (p.P) {
+    case 1: return launch_update_rows_t<1, VEC>(p, s);
+    case 2: return launch_update_rows_t<2, VEC>(p, s);
+    case 3: return launch_update_rows_t<3, VEC>(p, s);
+    case 4: return launch_update_rows_t<4, VEC>(p, s);
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
 }
 
 template <int P, int C, bool ACC, bool VEC>
@@ -837,6 +935,17 @@ int launch_staged(const StagedPlan& p, void* stream) {
   for (int q = 0; q < p.nl && vec; ++q) vec = aligned16(p.adst[q].ptr) && aligned16(p.adst[q].stripe_stride);
   for (int u = 0; u < p.nn && vec; ++u) vec = aligned16(p.bdst[u].ptr) && aligned16(p.bdst[u].stripe_stride);
   return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
+}
+
+int launch_update_rows(const UpdRowsPlan& p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.P < 1 || p.P > kMaxOut || p.nrows < 1 || p.nrows > kMaxSrc || (!p.rows && p.nrows != 1))
+    return static_cast<int>(hipErrorInvalidValue);
+  bool vec = aligned16(p.half);
+  for (const RowRef* r : {&p.old_row, &p.new_row})
+    vec = vec && aligned16(r->ptr) && aligned16(r->stripe_stride);
+  for (int q = 0; q < p.P && vec; ++q) vec = aligned16(p.dst[q].ptr) && aligned16(p.dst[q].stripe_stride);
+  return vec ? launch_update_rows_p<true>(p, s) : launch_update_rows_p<false>(p, s);
 }
 
 int launch_rows(const RowsPlan& p, void* stream) {

@@ -56,9 +56,11 @@ struct Batch {
   uint8_t* host = nullptr;      // pinned staging, compact [stripe][shard][size]
   uint8_t* host_dev = nullptr;  // its device address (zero-copy batches)
   uint8_t* dev = nullptr;
+  int32_t* rows = nullptr;      // pinned, mapped: Update's data row per slot
+  int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
   hipStream_t stream = nullptr;
   State state = FREE;
-  int key = -1;  // 0: encode, 1 + k: reconst_one(k)
+  int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows)
   size_t reserved = 0, filled = 0, released = 0;
   uint64_t gen = 0;
   int err = 0;
@@ -87,20 +89,32 @@ struct xrs_queue {
   std::thread worker[kMaxWorkers];
   int n_workers = 2, n_batches = 4;
 
+  // One copy between a caller's buffer and its staged stripe: `len` bytes at
+  // staging row `row` (row * size + off) <-> host + off.
+  struct Piece {
+    uint8_t* host;
+    int row;
+    size_t off, len;
+  };
+
   void run(int i);
   void work();
-  int submit(int key, uint8_t* const* vects, int n);
+  int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1);
 };
 
 void xrs_queue::run(int i) {
   Batch& bt = b[i];
   const size_t n = bt.reserved;
   // Encode: only the data rows go up and only the parity rows come back (one
-  // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back.
-  const size_t up_off = 0, up_len = bt.key == 0 ? static_cast<size_t>(d) * size : stripe_bytes;
-  const size_t dn_off = bt.key == 0 ? static_cast<size_t>(d) * size
-                                    : static_cast<size_t>(bt.key - 1) * size;
-  const size_t dn_len = bt.key == 0 ? static_cast<size_t>(p) * size : size;
+  // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back;
+  // Update(row): parity rows, old and new up (rows [0, p+2)), parity back.
+  const bool enc = bt.key == 0, upd = bt.key > d;
+  const size_t up_off = 0;
+  const size_t up_len = enc ? static_cast<size_t>(d) * size
+                            : upd ? static_cast<size_t>(p + 2) * size : stripe_bytes;
+  const size_t dn_off = enc ? static_cast<size_t>(d) * size
+                            : upd ? 0 : static_cast<size_t>(bt.key - 1) * size;
+  const size_t dn_len = enc || upd ? static_cast<size_t>(p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
   uint8_t* base = zc ? bt.host_dev : bt.dev;
   int e = 0;
@@ -108,9 +122,15 @@ void xrs_queue::run(int i) {
                               n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
   if (!e) {
-    e = bt.key == 0 ? xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream)
-                    : xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n,
-                                                  bt.key - 1, bt.stream);
+    if (enc)
+      e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
+    else if (upd)  // one launch for every row: each stripe carries its own
+      e = xrs_update_rows_batched(codec, base + static_cast<size_t>(p) * size, stripe_bytes,
+                                  base + static_cast<size_t>(p + 1) * size, stripe_bytes, size,
+                                  bt.rows_dev, base, size, stripe_bytes, n, bt.stream);
+    else
+      e = xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n, bt.key - 1,
+                                      bt.stream);
   }
   if (!e && !zc &&
       hipMemcpy2DAsync(bt.host + dn_off, stripe_bytes, bt.dev + dn_off, stripe_bytes, dn_len, n,
@@ -175,30 +195,8 @@ void xrs_queue::work() {
   }
 }
 
-int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
-  if (!vects || n != d + p) return XRS_ERR_ILLEGAL_VECTS;
-  for (int i = 0; i < n; ++i)
-    if (!vects[i]) return XRS_ERR_INVALID_ARG;
-  std::vector<std::pair<int, int>> in, out;  // (shard, 0 a / 1 b / 2 whole)
-  if (key == 0) {
-    for (int j = 0; j < d; ++j) in.push_back({j, 2});
-    for (int r = 0; r < p; ++r) out.push_back({d + r, 2});
-  } else {
-    const int k = key - 1;
-    std::vector<int> a_need;
-    int bi = 0;
-    const int e = xrs_detail::need_set(codec, k, &a_need, &bi);
-    if (e) return e;
-    for (int m = 0; m < d; ++m) in.push_back({m == k ? d : m, 1});
-    in.push_back({bi, 1});
-    for (int a : a_need) in.push_back({a, 0});
-    out.push_back({k, 2});
-  }
-  const size_t half = size / 2;
-  auto piece = [&](const std::pair<int, int>& pc, size_t* off, size_t* len) {
-    *off = pc.second == 1 ? half : 0;
-    *len = pc.second == 2 ? size : half;
-  };
+int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out,
+                      int row) {
   int bi;
   size_t slot;
   uint64_t gen;
@@ -242,11 +240,9 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
   }
   Batch& bt = b[bi];
   uint8_t* st = bt.host + slot * stripe_bytes;
-  for (auto& pc : in) {
-    size_t off, len;
-    piece(pc, &off, &len);
-    std::memcpy(st + static_cast<size_t>(pc.first) * size + off, vects[pc.first] + off, len);
-  }
+  if (row >= 0) bt.rows[slot] = row;
+  for (const Piece& pc : in)
+    std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
   int err;
   {
     std::unique_lock<std::mutex> lk(mu);
@@ -257,11 +253,8 @@ int xrs_queue::submit(int key, uint8_t* const* vects, int n) {
     err = bt.err;
   }
   if (!err)
-    for (auto& pc : out) {
-      size_t off, len;
-      piece(pc, &off, &len);
-      std::memcpy(vects[pc.first] + off, st + static_cast<size_t>(pc.first) * size + off, len);
-    }
+    for (const Piece& pc : out)
+      std::memcpy(pc.host + pc.off, st + static_cast<size_t>(pc.row) * size + pc.off, pc.len);
   {
     std::lock_guard<std::mutex> lk(mu);
     if (++bt.released == bt.reserved) {
@@ -288,7 +281,9 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   q->p = xrs_detail::codec_p(codec);
   q->device = dev;
   q->size = size;
-  q->stripe_bytes = static_cast<size_t>(q->d + q->p) * size;
+  // A staged stripe holds d+p vects (Encode, ReconstOne) or p parity + old +
+  // new (Update): p+2 rows, more than d+p only when d == 1.
+  q->stripe_bytes = static_cast<size_t>(std::max(q->d + q->p, q->p + 2)) * size;
   q->max_batch = std::max<size_t>(
       1, std::min(max_batch_stripes ? max_batch_stripes : SIZE_MAX, kMaxBatchBytes / q->stripe_bytes));
   q->max_wait = std::chrono::microseconds(max_wait_us);
@@ -311,6 +306,12 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     }
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, bt.host, 0) == hipSuccess) bt.host_dev = static_cast<uint8_t*>(dp);
+    if (hipHostMalloc(&bt.rows, q->max_batch * sizeof(int32_t), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(&dp, bt.rows, 0) != hipSuccess) {
+      e = XRS_ERR_HIP;
+      break;
+    }
+    bt.rows_dev = static_cast<int32_t*>(dp);
   }
   if (prev >= 0) (void)hipSetDevice(prev);
   if (e) {
@@ -343,22 +344,69 @@ void xrs_queue_free(xrs_queue* q) {
     if (bt.stream) (void)hipStreamDestroy(bt.stream);
     if (bt.dev) (void)hipFree(bt.dev);
     if (bt.host) (void)hipHostFree(bt.host);
+    if (bt.rows) (void)hipHostFree(bt.rows);
   }
   if (prev >= 0) (void)hipSetDevice(prev);
   delete q;
 }
 
-// xrs.go:103 Encode, coalesced with concurrent callers.
+// xrs.go:103 Encode, coalesced with concurrent callers: data rows in,
+// parity rows out.
 int xrs_queue_encode(xrs_queue* q, uint8_t* const* vects, int n) {
   if (!q) return XRS_ERR_INVALID_ARG;
-  return q->submit(0, vects, n);
+  if (!vects || n != q->d + q->p) return XRS_ERR_ILLEGAL_VECTS;
+  for (int i = 0; i < n; ++i)
+    if (!vects[i]) return XRS_ERR_INVALID_ARG;
+  std::vector<xrs_queue::Piece> in, out;
+  for (int j = 0; j < q->d; ++j) in.push_back({vects[j], j, 0, q->size});
+  for (int r = 0; r < q->p; ++r) out.push_back({vects[q->d + r], q->d + r, 0, q->size});
+  return q->submit(0, in, out);
 }
 
-// xrs.go:175 ReconstOne, coalesced (only the GetNeedVects set is copied).
+// xrs.go:175 ReconstOne, coalesced: only the GetNeedVects set is copied in
+// (b-halves of the d survivors and of parity bi, a-halves of aNeed), vect k
+// out.
 int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (k < 0 || k >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
-  return q->submit(1 + k, vects, n);
+  if (!vects || n != q->d + q->p) return XRS_ERR_ILLEGAL_VECTS;
+  for (int i = 0; i < n; ++i)
+    if (!vects[i]) return XRS_ERR_INVALID_ARG;
+  std::vector<int> a_need;
+  int bi = 0;
+  const int e = xrs_detail::need_set(q->codec, k, &a_need, &bi);
+  if (e) return e;
+  const size_t half = q->size / 2;
+  std::vector<xrs_queue::Piece> in, out;
+  for (int m = 0; m < q->d; ++m) {
+    const int h = m == k ? q->d : m;
+    in.push_back({vects[h], h, half, half});
+  }
+  in.push_back({vects[bi], bi, half, half});
+  for (int a : a_need) in.push_back({vects[a], a, 0, half});
+  out.push_back({vects[k], k, 0, q->size});
+  return q->submit(1 + k, in, out);
+}
+
+// xrs.go:324 Update(oldData, newData, row, parity), coalesced across rows
+// (each staged stripe carries its own row: update_rows kernel): staged rows
+// [0, p) parity, p old, p+1 new; parity out.
+int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_data, int row,
+                     uint8_t* const* parity, int n_parity) {
+  if (!q) return XRS_ERR_INVALID_ARG;
+  if (row < 0 || row >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (!parity || n_parity != q->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!old_data || !new_data) return XRS_ERR_INVALID_ARG;
+  for (int r = 0; r < n_parity; ++r)
+    if (!parity[r]) return XRS_ERR_INVALID_ARG;
+  std::vector<xrs_queue::Piece> in, out;
+  for (int r = 0; r < q->p; ++r) {
+    in.push_back({parity[r], r, 0, q->size});
+    out.push_back({parity[r], r, 0, q->size});
+  }
+  in.push_back({const_cast<uint8_t*>(old_data), q->p, 0, q->size});
+  in.push_back({const_cast<uint8_t*>(new_data), q->p + 1, 0, q->size});
+  return q->submit(1 + q->d, in, out, row);
 }
 
 size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }

@@ -92,9 +92,30 @@ struct StagedPlan {
   uint64_t n_stripes;
 };
 
+// "update_rows" kernel: Update (xrs.go:324) where every stripe names its own
+// data row (a batch of small writes to different shards):
+//   r = rows[s] - row0 (stripes with r outside [0, nrows) are skipped),
+//   delta = old ^ new,
+//   dst_q[o]   ^= tab[r][q] * delta[o]
+//   dst_q[H+o] ^= tab[r][q] * delta[H+o]  ^  (pbq[r] == q ? delta[o] : 0)
+struct UpdRowsPlan {
+  int P;      // outputs (<= kMaxOut)
+  int nrows;  // data rows covered by this launch (<= kMaxSrc), starting at row0
+  int row0;
+  GfTab tab[kMaxSrc][kMaxOut];
+  int8_t pbq[kMaxSrc];  // output whose b-half takes row r's delta a-half, or -1
+  RowRef old_row, new_row;
+  RowRef dst[kMaxOut];
+  uint64_t rows;  // device-readable address of n_stripes int32 data rows;
+                  // 0: every stripe uses row0 (nrows == 1)
+  uint64_t half;
+  uint64_t n_stripes;
+};
+
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.
 int launch_pair(const PairPlan& plan, void* stream);
 int launch_rows(const RowsPlan& plan, void* stream);
 int launch_staged(const StagedPlan& plan, void* stream);
+int launch_update_rows(const UpdRowsPlan& plan, void* stream);
 
 }  // namespace xrs

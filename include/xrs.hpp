@@ -159,4 +159,48 @@ class XRS {
   std::map<int, std::vector<int>> xorset_;
 };
 
+// Batching queue over a codec (xrs_queue_*): the same Encode / ReconstOne /
+// Update methods, callable from many threads at once; concurrent calls are
+// coalesced into device batches (one per vect size `size`).
+class Queue {
+ public:
+  static Error New(const XRS& x, size_t size, std::unique_ptr<Queue>* out,
+                   size_t max_batch_stripes = 1024, int max_wait_us = 50) {
+    xrs_queue* q = nullptr;
+    const int rc = xrs_queue_new(x.codec(), size, max_batch_stripes, max_wait_us, &q);
+    if (rc) return make_error(rc, static_cast<long long>(size));
+    out->reset(new Queue(q, size));
+    return {};
+  }
+  ~Queue() { xrs_queue_free(q_); }  // calls still in flight complete first
+  Queue(const Queue&) = delete;
+  Queue& operator=(const Queue&) = delete;
+
+  // xrs.go:103
+  Error Encode(std::vector<Slice> vects) {
+    auto p = ptrs(vects);
+    return make_error(xrs_queue_encode(q_, p.data(), static_cast<int>(p.size())),
+                      static_cast<long long>(size_));
+  }
+  Error Encode(Vects& vects) { return Encode(slices(vects)); }
+  // xrs.go:175
+  Error ReconstOne(std::vector<Slice> vects, int k) {
+    auto p = ptrs(vects);
+    return make_error(xrs_queue_reconst_one(q_, p.data(), static_cast<int>(p.size()), k), k);
+  }
+  Error ReconstOne(Vects& vects, int k) { return ReconstOne(slices(vects), k); }
+  // xrs.go:324
+  Error Update(const Vect& old_data, const Vect& new_data, int row, std::vector<Slice> parity) {
+    auto p = ptrs(parity);
+    return make_error(xrs_queue_update(q_, old_data.data(), new_data.data(), row, p.data(),
+                                       static_cast<int>(p.size())),
+                      row);
+  }
+
+ private:
+  Queue(xrs_queue* q, size_t size) : q_(q), size_(size) {}
+  xrs_queue* q_;
+  size_t size_;
+};
+
 }  // namespace xrs

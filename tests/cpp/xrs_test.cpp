@@ -5,11 +5,13 @@
 //   xrs_test --cpu   host-logic tests only (no GPU needed)
 //   xrs_test         all tests (needs the MI355X)
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 
 #include "xrs.hpp"
 
@@ -239,6 +241,45 @@ static void TestXRS_Replace() {
   testReplace(kData, kParity, kShard, 1024, false);
 }
 
+// Not in the reference: the batching queue from 16 threads, each checking its
+// own stripes against the synchronous calls (Encode, Update of random rows,
+// ReconstOne), then the queue destroyed while nothing is in flight.
+static void TestQueue_Concurrent() {
+  auto x = must_new(kData, kParity);
+  std::unique_ptr<xrs::Queue> q;
+  if (Error e = xrs::Queue::New(*x, kShard, &q, 64, 100)) FATAL("Queue::New: %s", e.msg.c_str());
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 16; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937_64 r(100 + t);
+      Vects v = new_shard_matrix(kData + kParity, kShard);
+      for (int j = 0; j < kData; ++j) fill_random(r, v[j]);
+      Vects ref = v;
+      if (q->Encode(v) || x->Encode(ref) || v != ref) ++bad;
+      for (int i = 0; i < 20; ++i) {
+        const int row = static_cast<int>(r() % kData);
+        Vect nd(kShard);
+        fill_random(r, nd);
+        auto pv = xrs::slices(v, kData), pr = xrs::slices(ref, kData);
+        if (q->Update(v[row], nd, row, pv) || x->Update(ref[row], nd, row, pr)) ++bad;
+        v[row] = nd;
+        ref[row] = nd;
+        if (v != ref) ++bad;
+        const int k = static_cast<int>(r() % kData);
+        Vects w = v;
+        std::fill(w[k].begin(), w[k].end(), 0);
+        if (q->ReconstOne(w, k) || w[k] != v[k]) ++bad;
+      }
+    });
+  for (auto& t : th) t.join();
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+  Vects par = new_shard_matrix(kParity, kShard);
+  if (Error e = q->Update(Vect(kShard), Vect(kShard), kData, xrs::slices(par));
+      !e || e.msg != "illegal data index: 12")
+    FATAL("Update(row=d): got \"%s\"", e.msg.c_str());
+}
+
 int main(int argc, char** argv) {
   const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
   struct T {
@@ -254,6 +295,7 @@ int main(int argc, char** argv) {
       {"TestXRS_Reconst", TestXRS_Reconst, true},
       {"TestXRS_Update", TestXRS_Update, true},
       {"TestXRS_Replace", TestXRS_Replace, true},
+      {"TestQueue_Concurrent", TestQueue_Concurrent, true},
   };
   for (const T& t : tests) {
     if (cpu_only && t.gpu) continue;

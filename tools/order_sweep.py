@@ -37,6 +37,8 @@ def main():
     cases = []
     staged = os.environ.get("CASES") == "staged"
     sizes = ((4096, 65536), (1 << 20, 512))
+    if os.environ.get("SIZES"):  # e.g. SIZES=4128,8192: batches of ~4 GiB
+        sizes = tuple((int(v), (4 << 30) // (16 * int(v))) for v in os.environ["SIZES"].split(","))
     if os.environ.get("CASES") == "staged":
         sizes = ((4096, 65536), (64 << 10, 4096), (1 << 20, 256), (8 << 20, 32))
     for size, n in sizes:

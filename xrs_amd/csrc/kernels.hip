@@ -144,6 +144,7 @@ struct PairArgs {
   uint64_t half;    // H
   uint64_t chunks;  // lanes per stripe
   uint64_t total;   // n_stripes * chunks
+  uint64_t off0;    // first byte of each half this launch covers
 };
 
 template <int P, int W>
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> 
   const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
   uint32_t acc_a[P][W], acc_b[P][W];
@@ -302,6 +303,7 @@ struct RowsArgs {
   uint64_t len;
   uint64_t chunks;
   uint64_t total;
+  uint64_t off0;
 };
 
 template <int R, int W>
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
   const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
 
   uint32_t acc[R][W];
@@ -439,7 +441,7 @@ struct StagedArgs {
   uint32_t bstore;
   int nd, na, nb, nl, nn, nr;
   BlockOrder order;
-  uint64_t half, chunks, total;
+  uint64_t half, chunks, total, off0;
 };
 
 // acc ^= abar(mask): wave-uniform branches, the masks have few bits set.
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(kBlock) void staged_kernel(const StagedArgs<NL, NN,
   const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
   uint32_t xa[kStSrc][W], xb[kStSrc][W];
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
   uint32_t xa[kStSrc][W], al[L1][W], rx[kStOut][W], ob[N1][W];
@@ -611,7 +613,7 @@ struct UpdRowsArgs {
   const int32_t* rows;
   int row0, nrows;
   BlockOrder order;
-  uint64_t half, chunks, total;
+  uint64_t half, chunks, total, off0;
 };
 
 template <int P, bool VEC>
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P
   const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = (gid - stripe * a.chunks) * (4 * W);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
   // rows == nullptr: one row for the whole batch (plain Update), table 0.
   const int r = a.rows ? a.rows[stripe] - a.row0 : 0;
@@ -666,8 +668,9 @@ enum class Shape { kPair, kRows, kStaged };
 // K per kernel shape and half-vect length, from interleaved medians of every
 // order on MI355X (profiles/r01_mapprobe2.log, r01_mapprobe3.log):
 //  * pair (Encode/Update/Replace): K = 32 is best or within 1% at 4 KiB-8 MiB;
-//  * rows (ReconstOne): 4 KiB vects want one range per XCD (K = nblk/8),
-//    8-128 KiB vects the plain order, >= 512 KiB vects K = half / 8 KiB up
+//  * rows (ReconstOne): vects up to 8 KiB want one range per XCD (K =
+//    nblk/8; 4,128-B vects +12%, 6 KiB +7%: profiles/r01_order_sweep_sizes.log),
+//    16-128 KiB vects the plain order, >= 512 KiB vects K = half / 8 KiB up
 //    to 256 (1 MiB: 64, 8 MiB: 256; profiles/r01_order_sweep.log);
 //  * staged (general Reconst): 4 KiB vects one range per XCD (+6-7% over
 //    K = 32), 512 KiB-2 MiB vects K = 128, >= 2 MiB vects the plain order
@@ -691,7 +694,7 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
       else if (len < (1u << 20)) o.k = 128;
       break;  // half >= 1 MiB: plain order
     case Shape::kRows:
-      if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
+      if (len <= 4096) o.k = static_cast<uint32_t>(blocks / 8);
       else if (len >= (256u << 10)) o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 13));
       break;
   }
@@ -733,7 +736,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   a.nl = p.nl;
   a.nn = p.nn;
   a.half = p.half;
-  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.off0 = p.off0;
+  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
@@ -791,7 +795,8 @@ int launch_update_rows_t(const UpdRowsPlan& p, hipStream_t stream) {
   a.row0 = p.row0;
   a.nrows = p.nrows;
   a.half = p.half;
-  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.off0 = p.off0;
+  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
@@ -830,7 +835,8 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
     if (p.pb[c] >= 0) a.pbmask[p.pb[c]] |= 1u << c;
   a.n_src = n;
   a.half = p.half;
-  a.chunks = VEC ? p.half / 16 : (p.half + 3) / 4;
+  a.off0 = p.off0;
+  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
@@ -878,7 +884,8 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   a.nm = p.NM;
   a.nx = p.NX;
   a.len = p.len;
-  a.chunks = VEC ? p.len / 16 : (p.len + 3) / 4;
+  a.off0 = p.off0;
+  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
@@ -912,52 +919,88 @@ int launch_rows_r(const RowsPlan& p, hipStream_t s) {
   }
 }
 
+// Each half (or row) of `len` bytes runs as [0, bulk) on the 16-byte kernels
+// and [bulk, len) on the byte-granular ones (bulk = len rounded down to 16).
+// MI355X executes global dwordx4 accesses at any byte alignment (the
+// runtime's unaligned access mode): exact, and 3-9% slower than aligned ones
+// (tools/unaligned_probe.hip, profiles/r01_unaligned_probe.log), so neither
+// misaligned rows / strides nor a ragged length force the byte path any more
+// (4-5x slower: profiles/r01_odd_probe.log).  XRS_UNALIGNED_VEC=0 restores
+// the strict rule for A/B runs: 16-byte kernels only when every row, stride
+// and len is 16-byte aligned.
+template <class Plan, class F>
+int split_launch(Plan p, uint64_t len, bool aligned, F launch) {
+  const char* e = std::getenv("XRS_UNALIGNED_VEC");
+  uint64_t bulk = len & ~uint64_t(15);
+  if (e && e[0] == '0' && !(aligned && bulk == len)) bulk = 0;
+  int rc = 0;
+  if (bulk) {
+    p.off0 = 0;
+    p.end = bulk;
+    rc = launch(p, true);
+  }
+  if (!rc && len > bulk) {
+    p.off0 = bulk;
+    p.end = len;
+    rc = launch(p, false);
+  }
+  return rc;
+}
+
+bool row_aligned(const RowRef& r) { return aligned16(r.ptr) && aligned16(r.stripe_stride); }
+
 }  // namespace
 
-int launch_pair(const PairPlan& p, void* stream) {
+int launch_pair(const PairPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.P < 1 || p.P > kMaxOut || p.C < 0 || p.C > kMaxSrc) return static_cast<int>(hipErrorInvalidValue);
-  bool vec = aligned16(p.half);
-  for (int c = 0; c < p.C && vec; ++c) vec = aligned16(p.src[c].ptr) && aligned16(p.src[c].stripe_stride);
-  for (int r = 0; r < p.P && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
-  if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
-  return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
+  if (p0.P < 1 || p0.P > kMaxOut || p0.C < 0 || p0.C > kMaxSrc) return static_cast<int>(hipErrorInvalidValue);
+  bool al = true;
+  for (int c = 0; c < p0.C; ++c) al = al && row_aligned(p0.src[c]);
+  for (int r = 0; r < p0.P; ++r) al = al && row_aligned(p0.dst[r]);
+  return split_launch(p0, p0.half, al, [s](const PairPlan& p, bool vec) {
+    if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
+    return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
+  });
 }
 
-int launch_staged(const StagedPlan& p, void* stream) {
+int launch_staged(const StagedPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.nd < 1 || p.nd > p.na || p.nd > p.nb || p.na > kStSrc || p.nb > kStSrc || p.nl < 0 ||
-      p.nl > kStOut || p.nn < 0 || p.nn > kStOut)
+  if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStSrc || p0.nl < 0 ||
+      p0.nl > kStOut || p0.nn < 0 || p0.nn > kStOut)
     return static_cast<int>(hipErrorInvalidValue);
-  bool vec = aligned16(p.half);
-  for (int m = 0; m < p.na && vec; ++m) vec = aligned16(p.asrc[m].ptr) && aligned16(p.asrc[m].stripe_stride);
-  for (int m = 0; m < p.nb && vec; ++m) vec = aligned16(p.bsrc[m].ptr) && aligned16(p.bsrc[m].stripe_stride);
-  for (int q = 0; q < p.nl && vec; ++q) vec = aligned16(p.adst[q].ptr) && aligned16(p.adst[q].stripe_stride);
-  for (int u = 0; u < p.nn && vec; ++u) vec = aligned16(p.bdst[u].ptr) && aligned16(p.bdst[u].stripe_stride);
-  return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
+  bool al = true;
+  for (int m = 0; m < p0.na; ++m) al = al && row_aligned(p0.asrc[m]);
+  for (int m = 0; m < p0.nb; ++m) al = al && row_aligned(p0.bsrc[m]);
+  for (int q = 0; q < p0.nl; ++q) al = al && row_aligned(p0.adst[q]);
+  for (int u = 0; u < p0.nn; ++u) al = al && row_aligned(p0.bdst[u]);
+  return split_launch(p0, p0.half, al, [s](const StagedPlan& p, bool vec) {
+    return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
+  });
 }
 
-int launch_update_rows(const UpdRowsPlan& p, void* stream) {
+int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.P < 1 || p.P > kMaxOut || p.nrows < 1 || p.nrows > kMaxSrc || (!p.rows && p.nrows != 1))
+  if (p0.P < 1 || p0.P > kMaxOut || p0.nrows < 1 || p0.nrows > kMaxSrc || (!p0.rows && p0.nrows != 1))
     return static_cast<int>(hipErrorInvalidValue);
-  bool vec = aligned16(p.half);
-  for (const RowRef* r : {&p.old_row, &p.new_row})
-    vec = vec && aligned16(r->ptr) && aligned16(r->stripe_stride);
-  for (int q = 0; q < p.P && vec; ++q) vec = aligned16(p.dst[q].ptr) && aligned16(p.dst[q].stripe_stride);
-  return vec ? launch_update_rows_p<true>(p, s) : launch_update_rows_p<false>(p, s);
+  bool al = row_aligned(p0.old_row) && row_aligned(p0.new_row);
+  for (int q = 0; q < p0.P; ++q) al = al && row_aligned(p0.dst[q]);
+  return split_launch(p0, p0.half, al, [s](const UpdRowsPlan& p, bool vec) {
+    return vec ? launch_update_rows_p<true>(p, s) : launch_update_rows_p<false>(p, s);
+  });
 }
 
-int launch_rows(const RowsPlan& p, void* stream) {
+int launch_rows(const RowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.R < 1 || p.R > kMaxOut || p.NM < 0 || p.NM > kMaxSrc || p.NX < 0 || p.NX > kMaxXor)
+  if (p0.R < 1 || p0.R > kMaxOut || p0.NM < 0 || p0.NM > kMaxSrc || p0.NX < 0 || p0.NX > kMaxXor)
     return static_cast<int>(hipErrorInvalidValue);
-  bool vec = aligned16(p.len);
-  for (int m = 0; m < p.NM && vec; ++m) vec = aligned16(p.msrc[m].ptr) && aligned16(p.msrc[m].stripe_stride);
-  for (int x = 0; x < p.NX && vec; ++x) vec = aligned16(p.xsrc[x].ptr) && aligned16(p.xsrc[x].stripe_stride);
-  for (int r = 0; r < p.R && vec; ++r) vec = aligned16(p.dst[r].ptr) && aligned16(p.dst[r].stripe_stride);
-  if (p.acc) return vec ? launch_rows_r<true, true>(p, s) : launch_rows_r<true, false>(p, s);
-  return vec ? launch_rows_r<false, true>(p, s) : launch_rows_r<false, false>(p, s);
+  bool al = true;
+  for (int m = 0; m < p0.NM; ++m) al = al && row_aligned(p0.msrc[m]);
+  for (int x = 0; x < p0.NX; ++x) al = al && row_aligned(p0.xsrc[x]);
+  for (int r = 0; r < p0.R; ++r) al = al && row_aligned(p0.dst[r]);
+  return split_launch(p0, p0.len, al, [s](const RowsPlan& p, bool vec) {
+    if (p.acc) return vec ? launch_rows_r<true, true>(p, s) : launch_rows_r<true, false>(p, s);
+    return vec ? launch_rows_r<false, true>(p, s) : launch_rows_r<false, false>(p, s);
+  });
 }
 
 }  // namespace xrs

@@ -51,6 +51,7 @@ struct PairPlan {
   bool encode12;       // pb follows the 12+4 XORSet (source c = data c): hot kernel
   uint64_t half;       // H = size/2 bytes
   uint64_t n_stripes;
+  uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_pair)
 };
 
 struct RowsPlan {
@@ -65,6 +66,7 @@ struct RowsPlan {
   RowRef dst[kMaxOut];
   uint64_t len;  // bytes per row
   uint64_t n_stripes;
+  uint64_t off0, end;  // byte range [off0, end) of each row (set by launch_rows)
 };
 
 // "staged" kernel: the general Reconst (xrs.go:236-301) in one pass, each of
@@ -90,6 +92,7 @@ struct StagedPlan {
   uint32_t nmask[kStOut];  // abar mask XORed into output u
   uint64_t half;
   uint64_t n_stripes;
+  uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_staged)
 };
 
 // "update_rows" kernel: Update (xrs.go:324) where every stripe names its own
@@ -110,6 +113,7 @@ struct UpdRowsPlan {
                   // 0: every stripe uses row0 (nrows == 1)
   uint64_t half;
   uint64_t n_stripes;
+  uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_update_rows)
 };
 
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.

@@ -753,7 +753,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   else late = late && blocks >= kLatencyGrid;
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   // (A compile-time survivor count, ND = 12, let the scheduler hoist the
-  // b-row loads: 225-232 VGPRs plus scratch.  Runtime nd only.)
+  // b-row loads: 225-232 VGPRs plus scratch, also with a sched_barrier
+  // between the a- and b-phases.  Runtime nd only.)
   if (late)
     hipLaunchKernelGGL((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, stream, a);

@@ -192,3 +192,40 @@ def test_queue_concurrent_update(size, d, p):
     with pytest.raises(xrs_amd.XRSError, match="illegal data index"):
         xrs_amd.XRSQueue(x, size).update(np.zeros(size, np.uint8), np.zeros(size, np.uint8), d,
                                          [np.zeros(size, np.uint8) for _ in range(p)])
+
+
+def test_batched_calls_from_threads_on_own_streams():
+    """One codec, 6 host threads, each launching batched Encode / ReconstOne /
+    Update on its own HIP stream and buffer at once (the codec is immutable
+    after xrs_new; batched calls share no staging): every result bit-exact."""
+    torch = pytest.importorskip("torch")
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    size, n = 4096, 300
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.Generator(np.random.PCG64(5000 + t))
+            host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+            ref = host.copy()
+            o.encode_batch(ref, size, n)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                dt = torch.from_numpy(host).cuda()
+                s = st.cuda_stream
+                for it in range(5):
+                    x.encode_batched(dt.data_ptr(), size, size, (D + P) * size, n, s)
+                    k = (t + it) % D
+                    dt[:, k].zero_()
+                    x.reconst_one_batched(dt.data_ptr(), size, size, (D + P) * size, n, k, s)
+                st.synchronize()
+                assert np.array_equal(dt.cpu().numpy(), ref), t
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]

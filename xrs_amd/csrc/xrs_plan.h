@@ -1,9 +1,11 @@
 // xrs_plan.h -- launch plans shared by the host planner (codec.cpp) and the
 // gfx950 kernels (kernels.hip).  Internal; not part of the C ABI.
 //
-// Two kernel shapes cover the whole xrs.go API surface:
+// Four kernel shapes cover the whole xrs.go API surface: "pair" and "rows"
+// below, the one-pass general Reconst ("staged", StagedPlan) and Update
+// ("update_rows", UpdRowsPlan).
 //
-//  * "pair" kernel  (Encode xrs.go:103, Replace :363, Update :324):
+//  * "pair" kernel  (Encode xrs.go:103, Replace :363):
 //      for every byte offset o of the a-half (H = size/2):
 //        dst_r[o]   (^)= sum_c coef[c][r] * src_c[o]
 //        dst_r[H+o] (^)= sum_c coef[c][r] * src_c[H+o]  ^  XOR_{c: pb[c]==r} src_c[o]

@@ -229,10 +229,14 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    # Every rank's time (one slot each, summed), so the max and the spread
+    # across ranks are both reported.
+    t = torch.zeros(world, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    t[rank] = elapsed
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    rank_seconds = [float(v) for v in t.cpu()]
+    elapsed_max = max(rank_seconds)
     total_bytes = world * args.steps * step_bytes
     value = total_bytes / elapsed_max / 2**30
 
@@ -288,6 +292,7 @@ def main():
                 "encode_shard_stride": enc_shard, "reconst_shard_stride": rec_shard,
                 "parallelism": f"stripe split x{world}, no collective",
             },
+            "rank_seconds": [round(v, 6) for v in rank_seconds],
             "kernels": kernels,
             "roofline": roofline,
             "cpu_baseline": cpu,

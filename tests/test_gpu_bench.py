@@ -53,3 +53,5 @@ def test_bench_two_ranks_contract():
     assert KEYS <= set(j)
     assert j["n_gpus"] == 2 and j["scaling"] == "weak" and j["value"] > 0
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
+    assert len(j["rank_seconds"]) == 2 and min(j["rank_seconds"]) > 0
+    assert abs(j["ms_per_step"] * j["steps"] / 1e3 - max(j["rank_seconds"])) < 1e-3

@@ -160,7 +160,7 @@ class XRS {
 };
 
 // Batching queue over a codec (xrs_queue_*): the same Encode / ReconstOne /
-// Update methods, callable from many threads at once; concurrent calls are
+// Reconst / Update methods, callable from many threads at once; concurrent calls are
 // coalesced into device batches (one per vect size `size`).
 class Queue {
  public:
@@ -189,6 +189,19 @@ class Queue {
     return make_error(xrs_queue_reconst_one(q_, p.data(), static_cast<int>(p.size()), k), k);
   }
   Error ReconstOne(Vects& vects, int k) { return ReconstOne(slices(vects), k); }
+  // xrs.go:236 (batches keyed by the (dpHas, need) pattern)
+  Error Reconst(std::vector<Slice> vects, const std::vector<int>& dp_has,
+                const std::vector<int>& need) {
+    auto p = ptrs(vects);
+    const int rc = xrs_queue_reconst(q_, p.data(), static_cast<int>(p.size()), dp_has.data(),
+                                     static_cast<int>(dp_has.size()), need.data(),
+                                     static_cast<int>(need.size()));
+    return make_error(rc, rc == XRS_ERR_SIZE_NOT_EVEN ? static_cast<long long>(size_)
+                                                      : (need.empty() ? 0 : need[0]));
+  }
+  Error Reconst(Vects& vects, const std::vector<int>& dp_has, const std::vector<int>& need) {
+    return Reconst(slices(vects), dp_has, need);
+  }
   // xrs.go:324
   Error Update(const Vect& old_data, const Vect& new_data, int row, std::vector<Slice> parity) {
     auto p = ptrs(parity);

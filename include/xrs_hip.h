@@ -193,7 +193,7 @@ int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
  * x.Encode / x.ReconstOne / x.Update) into device batches of up to
  * max_batch_stripes (capped at 64 MiB of staging) with one H2D, one kernel
  * and one D2H per batch; a batch holds calls of one kind (Encode, ReconstOne
- * of one k, or Update of any rows).  A batch runs when full, or max_wait_us after
+ * of one k, Reconst of one (dpHas, need) pattern, or Update of any rows).  A batch runs when full, or max_wait_us after
  * it opened once every reserved stripe is staged (at once when small and the
  * GPU is idle).  Each call blocks until its own stripe is done and has the
  * semantics of xrs_encode / xrs_reconst_one / xrs_update for vects of the
@@ -205,6 +205,12 @@ int xrs_queue_new(const xrs_codec *codec, size_t size, size_t max_batch_stripes,
 void xrs_queue_free(xrs_queue *q);
 int xrs_queue_encode(xrs_queue *q, uint8_t *const *vects, int n);
 int xrs_queue_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k);
+/* xrs.go:236 Reconst(vects, dpHas, needReconst), coalesced: calls with the
+ * same (dpHas, needReconst) share a batch, with the side effects of
+ * xrs_reconst; calls with invalid, repeated or overlapping indexes run as a
+ * plain xrs_reconst. */
+int xrs_queue_reconst(xrs_queue *q, uint8_t *const *vects, int n, const int *dp_has, int n_has,
+                      const int *need, int n_need);
 /* xrs.go:324 Update(oldData, newData, row, parity), coalesced. */
 int xrs_queue_update(xrs_queue *q, const uint8_t *old_data, const uint8_t *new_data, int row,
                      uint8_t *const *parity, int n_parity);

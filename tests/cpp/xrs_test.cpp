@@ -243,7 +243,8 @@ static void TestXRS_Replace() {
 
 // Not in the reference: the batching queue from 16 threads, each checking its
 // own stripes against the synchronous calls (Encode, Update of random rows,
-// ReconstOne), then the queue destroyed while nothing is in flight.
+// ReconstOne, two-loss Reconst), then the queue destroyed while nothing is in
+// flight.
 static void TestQueue_Concurrent() {
   auto x = must_new(kData, kParity);
   std::unique_ptr<xrs::Queue> q;
@@ -270,6 +271,17 @@ static void TestQueue_Concurrent() {
         Vects w = v;
         std::fill(w[k].begin(), w[k].end(), 0);
         if (q->ReconstOne(w, k) || w[k] != v[k]) ++bad;
+        // two lost (one data, one parity), both needed: queue vs sync call
+        const std::vector<int> lost = {k, kData + 1 + (i % (kParity - 1))};
+        std::vector<int> has;
+        for (int j = 0; j < kData + kParity; ++j)
+          if (!is_in(j, lost)) has.push_back(j);
+        Vects g1 = v, g2 = v;
+        for (int j : lost) {
+          std::fill(g1[j].begin(), g1[j].end(), 0x5a);
+          std::fill(g2[j].begin(), g2[j].end(), 0x5a);
+        }
+        if (q->Reconst(g1, has, lost) || x->Reconst(g2, has, lost) || g1 != g2) ++bad;
       }
     });
   for (auto& t : th) t.join();

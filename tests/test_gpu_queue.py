@@ -229,3 +229,43 @@ def test_batched_calls_from_threads_on_own_streams():
     for t in th:
         t.join()
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("size", [4096, 1030])
+def test_queue_reconst_patterns(size):
+    """xrs_queue_reconst from 12 threads over 3 loss patterns (batches keyed by
+    pattern), plus unclean calls (repeated index, need inside dpHas) that run
+    as plain xrs_reconst: every buffer, side effects included, equals the
+    oracle's."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=32, max_wait_us=200)
+    patterns = [([0, 1], [0, 1]), ([3, 13, 15], [3, 13]), ([2, 5, 9, 14], [2, 5, 9, 14]),
+                ([7], [7, 7]), ([1, 4], [1, 2])]
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(6000 + t))
+        try:
+            for i in range(10):
+                lost, need = patterns[(t + i) % len(patterns)]
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+                o.encode(v)
+                has = [j for j in range(D + P) if j not in lost]
+                for j in lost:
+                    v[j][:] = 0x5A
+                a, b = [r.copy() for r in v], [r.copy() for r in v]
+                q.reconst(a, has, need)
+                o.reconst(b, has, need)
+                assert all(np.array_equal(s, u) for s, u in zip(a, b)), (t, i, lost, need)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    st = q.stats()
+    q.close()
+    assert not errors, errors[:3]
+    assert st["stripes"] > 0

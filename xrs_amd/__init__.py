@@ -104,6 +104,7 @@ def _load():
         "xrs_queue_encode": ([P, PP, I], I),
         "xrs_queue_reconst_one": ([P, PP, I, I], I),
         "xrs_queue_update": ([P, P, P, I, PP, I], I),
+        "xrs_queue_reconst": ([P, PP, I, IP, I, IP, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
         "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
@@ -414,6 +415,12 @@ class XRSQueue:
     def reconst_one(self, vects, need_reconst: int) -> None:
         _raise(self._call(_lib.xrs_queue_reconst_one, _ptrs(vects), len(vects),
                           int(need_reconst)), need_reconst)
+
+    def reconst(self, vects, dp_has, need_reconst) -> None:
+        rc = self._call(_lib.xrs_queue_reconst, _ptrs(vects), len(vects), _ints(dp_has),
+                        len(dp_has), _ints(need_reconst), len(need_reconst))
+        arg = self.size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
 
     def update(self, old_data, new_data, row: int, parity) -> None:
         _raise(self._call(_lib.xrs_queue_update, _ptr(old_data), _ptr(new_data), int(row),

@@ -60,7 +60,9 @@ struct Batch {
   int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
   hipStream_t stream = nullptr;
   State state = FREE;
-  int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows)
+  int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows),
+                 // 2 + d: reconst(pat_has, pat_need)
+  std::vector<int> pat_has, pat_need;  // Reconst pattern of the batch
   size_t reserved = 0, filled = 0, released = 0;
   uint64_t gen = 0;
   int err = 0;
@@ -99,7 +101,8 @@ struct xrs_queue {
 
   void run(int i);
   void work();
-  int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1);
+  int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1,
+             const std::vector<int>* has = nullptr, const std::vector<int>* need = nullptr);
 };
 
 void xrs_queue::run(int i) {
@@ -108,13 +111,14 @@ void xrs_queue::run(int i) {
   // Encode: only the data rows go up and only the parity rows come back (one
   // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back;
   // Update(row): parity rows, old and new up (rows [0, p+2)), parity back.
-  const bool enc = bt.key == 0, upd = bt.key > d;
+  const bool enc = bt.key == 0, upd = bt.key == 1 + d, rec = bt.key == 2 + d;
   const size_t up_off = 0;
   const size_t up_len = enc ? static_cast<size_t>(d) * size
                             : upd ? static_cast<size_t>(p + 2) * size : stripe_bytes;
   const size_t dn_off = enc ? static_cast<size_t>(d) * size
-                            : upd ? 0 : static_cast<size_t>(bt.key - 1) * size;
-  const size_t dn_len = enc || upd ? static_cast<size_t>(p) * size : size;
+                            : upd || rec ? 0 : static_cast<size_t>(bt.key - 1) * size;
+  const size_t dn_len = enc || upd ? static_cast<size_t>(p) * size
+                                   : rec ? static_cast<size_t>(d + p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
   uint8_t* base = zc ? bt.host_dev : bt.dev;
   int e = 0;
@@ -124,6 +128,10 @@ void xrs_queue::run(int i) {
   if (!e) {
     if (enc)
       e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
+    else if (rec)
+      e = xrs_reconst_batched(codec, base, size, size, stripe_bytes, n, bt.pat_has.data(),
+                              static_cast<int>(bt.pat_has.size()), bt.pat_need.data(),
+                              static_cast<int>(bt.pat_need.size()), bt.stream);
     else if (upd)  // one launch for every row: each stripe carries its own
       e = xrs_update_rows_batched(codec, base + static_cast<size_t>(p) * size, stripe_bytes,
                                   base + static_cast<size_t>(p + 1) * size, stripe_bytes, size,
@@ -196,7 +204,10 @@ void xrs_queue::work() {
 }
 
 int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out,
-                      int row) {
+                      int row, const std::vector<int>* has, const std::vector<int>* need) {
+  auto same_pattern = [&](const Batch& bt) {
+    return !has || (bt.pat_has == *has && bt.pat_need == *need);
+  };
   int bi;
   size_t slot;
   uint64_t gen;
@@ -209,7 +220,8 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
         cv_free.notify_all();
         return XRS_ERR_INVALID_ARG;
       }
-      if (open >= 0 && b[open].key == key && b[open].reserved < max_batch) break;
+      if (open >= 0 && b[open].key == key && b[open].reserved < max_batch && same_pattern(b[open]))
+        break;
       if (open >= 0) {  // different op or full: close it, the worker runs it
         b[open].state = CLOSED;
         open = -1;
@@ -228,6 +240,10 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       nb.reserved = nb.filled = nb.released = 0;
       nb.err = 0;
       nb.opened = Clock::now();
+      if (has) {
+        nb.pat_has = *has;
+        nb.pat_need = *need;
+      }
       open = f;
     }
     bi = open;
@@ -407,6 +423,52 @@ int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_d
   in.push_back({const_cast<uint8_t*>(old_data), q->p, 0, q->size});
   in.push_back({const_cast<uint8_t*>(new_data), q->p + 1, 0, q->size});
   return q->submit(1 + q->d, in, out, row);
+}
+
+// xrs.go:236 Reconst(vects, dpHas, needReconst), coalesced: calls with the
+// same (dpHas, needReconst) share a batch.  The survivors go up whole, and
+// every half the reference writes comes back: the a-halves of every vect not
+// in dpHas, the b-halves of surviving piggybacked parity (retrieveRS,
+// xrs.go:305-320) and of every needed vect.  A call whose indexes are not all
+// valid and distinct, or whose need overlaps dpHas, runs as a plain
+// xrs_reconst (the reference's partial side effects and toggling).
+int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_has, int n_has,
+                      const int* need, int n_need) {
+  if (!q) return XRS_ERR_INVALID_ARG;
+  if (n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] >= 0 && need[0] < q->d)  // xrs.go:238-240
+    return xrs_queue_reconst_one(q, vects, n, need[0]);
+  const int d = q->d, m = q->d + q->p;
+  if (!vects || n != m) return XRS_ERR_ILLEGAL_VECTS;
+  for (int i = 0; i < n; ++i)
+    if (!vects[i]) return XRS_ERR_INVALID_ARG;
+  std::vector<int> in_has(m, 0), in_need(m, 0);
+  bool clean = n_has >= d;
+  for (int i = 0; i < n_has && clean; ++i) {
+    clean = dp_has[i] >= 0 && dp_has[i] < m && !in_has[dp_has[i]];
+    if (clean) in_has[dp_has[i]] = 1;
+  }
+  for (int u = 0; u < n_need && clean; ++u) {
+    clean = need[u] >= 0 && need[u] < m && !in_has[need[u]] && !in_need[need[u]];
+    if (clean) in_need[need[u]] = 1;
+  }
+  if (!clean) return xrs_reconst(q->codec, vects, n, q->size, dp_has, n_has, need, n_need);
+  const size_t half = q->size / 2;
+  std::vector<xrs_queue::Piece> in, out;
+  for (int i = 0; i < m; ++i) {
+    if (in_has[i]) {
+      in.push_back({vects[i], i, 0, q->size});
+      int idx[256], len = 0;
+      if (i > d && xrs_xorset(q->codec, i, idx, 256, &len) == XRS_OK && len > 0)
+        out.push_back({vects[i], i, half, half});  // retrieveRS side effect
+    } else {
+      out.push_back({vects[i], i, 0, half});  // every lost a-half is rebuilt
+      if (in_need[i]) out.push_back({vects[i], i, half, half});
+    }
+  }
+  const std::vector<int> has(dp_has, dp_has + n_has), nd(need, need + n_need);
+  return q->submit(2 + d, in, out, -1, &has, &nd);
 }
 
 size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }

@@ -160,7 +160,7 @@ class XRS {
 };
 
 // Batching queue over a codec (xrs_queue_*): the same Encode / ReconstOne /
-// Reconst / Update methods, callable from many threads at once; concurrent calls are
+// Reconst / Update / Replace methods, callable from many threads at once; concurrent calls are
 // coalesced into device batches (one per vect size `size`).
 class Queue {
  public:
@@ -169,7 +169,7 @@ class Queue {
     xrs_queue* q = nullptr;
     const int rc = xrs_queue_new(x.codec(), size, max_batch_stripes, max_wait_us, &q);
     if (rc) return make_error(rc, static_cast<long long>(size));
-    out->reset(new Queue(q, size));
+    out->reset(new Queue(q, size, x.DataNum()));
     return {};
   }
   ~Queue() { xrs_queue_free(q_); }  // calls still in flight complete first
@@ -202,6 +202,20 @@ class Queue {
   Error Reconst(Vects& vects, const std::vector<int>& dp_has, const std::vector<int>& need) {
     return Reconst(slices(vects), dp_has, need);
   }
+  // xrs.go:363 (batches keyed by the rows set)
+  Error Replace(std::vector<Slice> data, const std::vector<int>& rows, std::vector<Slice> parity) {
+    auto d = ptrs(data);
+    auto p = ptrs(parity);
+    const int rc = xrs_queue_replace(q_, d.data(), rows.data(), static_cast<int>(rows.size()),
+                                     p.data(), static_cast<int>(p.size()));
+    long long arg = 0;
+    for (int r : rows)
+      if (r < 0 || r >= codec_d_) {
+        arg = r;
+        break;
+      }
+    return make_error(rc, arg);
+  }
   // xrs.go:324
   Error Update(const Vect& old_data, const Vect& new_data, int row, std::vector<Slice> parity) {
     auto p = ptrs(parity);
@@ -211,9 +225,10 @@ class Queue {
   }
 
  private:
-  Queue(xrs_queue* q, size_t size) : q_(q), size_(size) {}
+  Queue(xrs_queue* q, size_t size, int d) : q_(q), size_(size), codec_d_(d) {}
   xrs_queue* q_;
   size_t size_;
+  int codec_d_;
 };
 
 }  // namespace xrs

@@ -193,7 +193,8 @@ int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
  * x.Encode / x.ReconstOne / x.Update) into device batches of up to
  * max_batch_stripes (capped at 64 MiB of staging) with one H2D, one kernel
  * and one D2H per batch; a batch holds calls of one kind (Encode, ReconstOne
- * of one k, Reconst of one (dpHas, need) pattern, or Update of any rows).  A batch runs when full, or max_wait_us after
+ * of one k, Reconst of one (dpHas, need) pattern, Replace of one rows set,
+ * or Update of any rows).  A batch runs when full, or max_wait_us after
  * it opened once every reserved stripe is staged (at once when small and the
  * GPU is idle).  Each call blocks until its own stripe is done and has the
  * semantics of xrs_encode / xrs_reconst_one / xrs_update for vects of the
@@ -211,6 +212,9 @@ int xrs_queue_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k);
  * plain xrs_reconst. */
 int xrs_queue_reconst(xrs_queue *q, uint8_t *const *vects, int n, const int *dp_has, int n_has,
                       const int *need, int n_need);
+/* xrs.go:363 Replace(data, replaceRows, parity), coalesced per rows set. */
+int xrs_queue_replace(xrs_queue *q, uint8_t *const *data, const int *rows, int n,
+                      uint8_t *const *parity, int n_parity);
 /* xrs.go:324 Update(oldData, newData, row, parity), coalesced. */
 int xrs_queue_update(xrs_queue *q, const uint8_t *old_data, const uint8_t *new_data, int row,
                      uint8_t *const *parity, int n_parity);

@@ -282,6 +282,14 @@ static void TestQueue_Concurrent() {
           std::fill(g2[j].begin(), g2[j].end(), 0x5a);
         }
         if (q->Reconst(g1, has, lost) || x->Reconst(g2, has, lost) || g1 != g2) ++bad;
+        // Replace of two rows with fresh data: queue vs sync call
+        const std::vector<int> rr = {row, (row + 5) % kData};
+        Vects nd2 = new_shard_matrix(2, kShard);
+        for (auto& z : nd2) fill_random(r, z);
+        Vects pq(v.begin() + kData, v.end()), ps = pq;
+        if (q->Replace(xrs::slices(nd2), rr, xrs::slices(pq)) ||
+            x->Replace(xrs::slices(nd2), rr, xrs::slices(ps)) || pq != ps)
+          ++bad;
       }
     });
   for (auto& t : th) t.join();

@@ -269,3 +269,40 @@ def test_queue_reconst_patterns(size):
     q.close()
     assert not errors, errors[:3]
     assert st["stripes"] > 0
+
+
+def test_queue_replace_rows_sets():
+    """xrs_queue_replace from 10 threads over 3 rows sets (one batch per set):
+    parity bit-exact to the oracle; bad rows rejected before any write."""
+    size = 4096
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=32, max_wait_us=200)
+    sets = [[0], [1, 4, 7, 10], [11, 2, 5, 8, 3, 6, 9, 0]]
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(6500 + t))
+        try:
+            for i in range(8):
+                rows = sets[(t + i) % len(sets)]
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+                o.encode(v)
+                data = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in rows]
+                p1, p2 = [a.copy() for a in v[D:]], [a.copy() for a in v[D:]]
+                q.replace(data, rows, p1)
+                o.replace(data, rows, p2)
+                assert all(np.array_equal(a, b) for a, b in zip(p1, p2)), (t, i, rows)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(10)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    par = [np.zeros(size, np.uint8) for _ in range(P)]
+    with pytest.raises(xrs_amd.XRSError, match="illegal data index: 12"):
+        q.replace([np.zeros(size, np.uint8)], [12], par)
+    assert not any(a.any() for a in par)
+    q.close()
+    assert not errors, errors[:3]

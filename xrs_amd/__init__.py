@@ -105,6 +105,7 @@ def _load():
         "xrs_queue_reconst_one": ([P, PP, I, I], I),
         "xrs_queue_update": ([P, P, P, I, PP, I], I),
         "xrs_queue_reconst": ([P, PP, I, IP, I, IP, I], I),
+        "xrs_queue_replace": ([P, PP, IP, I, PP, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
         "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
@@ -421,6 +422,12 @@ class XRSQueue:
                         len(dp_has), _ints(need_reconst), len(need_reconst))
         arg = self.size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
         _raise(rc, arg)
+
+    def replace(self, data, replace_rows, parity) -> None:
+        rc = self._call(_lib.xrs_queue_replace, _ptrs(data), _ints(replace_rows),
+                        len(replace_rows), _ptrs(parity), len(parity))
+        bad = next((r for r in replace_rows if r < 0 or r >= self._codec.data_num), 0)
+        _raise(rc, bad)
 
     def update(self, old_data, new_data, row: int, parity) -> None:
         _raise(self._call(_lib.xrs_queue_update, _ptr(old_data), _ptr(new_data), int(row),

@@ -61,7 +61,7 @@ struct Batch {
   hipStream_t stream = nullptr;
   State state = FREE;
   int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows),
-                 // 2 + d: reconst(pat_has, pat_need)
+                 // 2 + d: reconst(pat_has, pat_need), 3 + d: replace(pat_has = rows)
   std::vector<int> pat_has, pat_need;  // Reconst pattern of the batch
   size_t reserved = 0, filled = 0, released = 0;
   uint64_t gen = 0;
@@ -111,14 +111,18 @@ void xrs_queue::run(int i) {
   // Encode: only the data rows go up and only the parity rows come back (one
   // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back;
   // Update(row): parity rows, old and new up (rows [0, p+2)), parity back.
-  const bool enc = bt.key == 0, upd = bt.key == 1 + d, rec = bt.key == 2 + d;
+  const bool enc = bt.key == 0, upd = bt.key == 1 + d, rec = bt.key == 2 + d,
+             rep = bt.key == 3 + d;
   const size_t up_off = 0;
-  const size_t up_len = enc ? static_cast<size_t>(d) * size
-                            : upd ? static_cast<size_t>(p + 2) * size : stripe_bytes;
+  // Replace(rows): parity rows [0, p) and the n data rows [p, p+n) up, parity back.
+  const size_t up_len = enc   ? static_cast<size_t>(d) * size
+                        : upd ? static_cast<size_t>(p + 2) * size
+                        : rep ? (p + bt.pat_has.size()) * size
+                              : stripe_bytes;
   const size_t dn_off = enc ? static_cast<size_t>(d) * size
-                            : upd || rec ? 0 : static_cast<size_t>(bt.key - 1) * size;
-  const size_t dn_len = enc || upd ? static_cast<size_t>(p) * size
-                                   : rec ? static_cast<size_t>(d + p) * size : size;
+                            : upd || rec || rep ? 0 : static_cast<size_t>(bt.key - 1) * size;
+  const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
+                                          : rec ? static_cast<size_t>(d + p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
   uint8_t* base = zc ? bt.host_dev : bt.dev;
   int e = 0;
@@ -128,6 +132,10 @@ void xrs_queue::run(int i) {
   if (!e) {
     if (enc)
       e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
+    else if (rep)
+      e = xrs_replace_batched(codec, base + static_cast<size_t>(p) * size, size, stripe_bytes,
+                              bt.pat_has.data(), static_cast<int>(bt.pat_has.size()), size, base,
+                              size, stripe_bytes, n, bt.stream);
     else if (rec)
       e = xrs_reconst_batched(codec, base, size, size, stripe_bytes, n, bt.pat_has.data(),
                               static_cast<int>(bt.pat_has.size()), bt.pat_need.data(),
@@ -469,6 +477,32 @@ int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_
   }
   const std::vector<int> has(dp_has, dp_has + n_has), nd(need, need + n_need);
   return q->submit(2 + d, in, out, -1, &has, &nd);
+}
+
+// xrs.go:363 Replace(data, replaceRows, parity), coalesced: calls with the
+// same rows share a batch (staged rows [0, p) parity, [p, p+n) data);
+// parity out.
+int xrs_queue_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n,
+                      uint8_t* const* parity, int n_parity) {
+  if (!q) return XRS_ERR_INVALID_ARG;
+  if (n < 1 || n > q->d) return XRS_ERR_ILLEGAL_VECTS;
+  if (!rows) return XRS_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (!parity || n_parity != q->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!data) return XRS_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (!data[i]) return XRS_ERR_INVALID_ARG;
+  for (int r = 0; r < n_parity; ++r)
+    if (!parity[r]) return XRS_ERR_INVALID_ARG;
+  std::vector<xrs_queue::Piece> in, out;
+  for (int r = 0; r < q->p; ++r) {
+    in.push_back({parity[r], r, 0, q->size});
+    out.push_back({parity[r], r, 0, q->size});
+  }
+  for (int i = 0; i < n; ++i) in.push_back({data[i], q->p + i, 0, q->size});
+  const std::vector<int> rv(rows, rows + n), none;
+  return q->submit(3 + q->d, in, out, -1, &rv, &none);
 }
 
 size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }

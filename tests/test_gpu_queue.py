@@ -306,3 +306,67 @@ def test_queue_replace_rows_sets():
     assert not any(a.any() for a in par)
     q.close()
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("d,p,size", [(12, 4, 4096), (6, 3, 1030), (10, 4, 65536)])
+def test_queue_mixed_ops_fuzz(d, p, size):
+    """16 threads issue random operations of every kind (Encode, ReconstOne,
+    Reconst over a few loss patterns, Update of any row, Replace over a few
+    rows sets) on one queue, so batches of different kinds and patterns
+    open and close under contention; every result equals the oracle's."""
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=16, max_wait_us=80)
+    rng0 = np.random.Generator(np.random.PCG64(77 + d))
+    patterns = []
+    for _ in range(3):
+        lost = [int(v) for v in rng0.permutation(d + p)[: int(rng0.integers(2, p + 1))]]
+        patterns.append((lost, lost[: max(2, len(lost) - 1)]))
+    row_sets = [[int(v) for v in rng0.permutation(d)[: int(rng0.integers(1, d + 1))]]
+                for _ in range(3)]
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(8000 + t))
+        try:
+            for i in range(10):
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d + p)]
+                o.encode(v)
+                a, b = [r.copy() for r in v], [r.copy() for r in v]
+                op = int(rng.integers(0, 5))
+                if op == 0:
+                    for r in a[d:]:
+                        r[:] = 0
+                    q.encode(a)
+                elif op == 1:
+                    k = int(rng.integers(0, d))
+                    a[k][:] = 0
+                    q.reconst_one(a, k)
+                elif op == 2:
+                    lost, need = patterns[int(rng.integers(0, len(patterns)))]
+                    has = [j for j in range(d + p) if j not in lost]
+                    for j in lost:
+                        a[j][:] = 0x11
+                        b[j][:] = 0x11
+                    q.reconst(a, has, need)
+                    o.reconst(b, has, need)
+                elif op == 3:
+                    row = int(rng.integers(0, d))
+                    new = rng.integers(0, 256, size=size, dtype=np.uint8)
+                    q.update(a[row], new, row, a[d:])
+                    o.update(b[row], new, row, b[d:])
+                else:
+                    rows = row_sets[int(rng.integers(0, len(row_sets)))]
+                    data = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in rows]
+                    q.replace(data, rows, a[d:])
+                    o.replace(data, rows, b[d:])
+                assert all(np.array_equal(s, u) for s, u in zip(a, b)), (t, i, op)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    q.close()
+    assert not errors, errors[:3]

@@ -160,6 +160,12 @@ int xrs_encode_host(const xrs_codec *codec, uint8_t *host_base, size_t size, siz
 /* ReconstOne(k) per stripe; only the GetNeedVects halves cross PCIe. */
 int xrs_reconst_one_host(const xrs_codec *codec, uint8_t *host_base, size_t size,
                          size_t shard_stride, size_t stripe_stride, size_t n_stripes, int k);
+/* xrs.go:236 Reconst(dpHas, need) over a host-resident batch (same layout
+ * rules; a clean call moves only the survivors up and the written halves
+ * back, with the reference's side effects). */
+int xrs_reconst_host(const xrs_codec *codec, uint8_t *host_base, size_t size, size_t shard_stride,
+                     size_t stripe_stride, size_t n_stripes, const int *dp_has, int n_has,
+                     const int *need, int n_need);
 void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */
 void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */

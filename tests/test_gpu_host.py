@@ -99,3 +99,39 @@ def test_host_zero_copy_inside_allocation(rng):
             assert np.array_equal(buf[a:a + size], v[i]), (s, i)
     assert xrs_amd.lib().xrs_host_device_pointer(ptr)
     xrs_amd.lib().xrs_host_free(ptr)
+
+
+@pytest.mark.parametrize("size,n", [(4096, 3000), (1026, 257), (1 << 20, 9)])
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
+def test_reconst_host_vs_oracle(rng, monkeypatch, size, n, mode):
+    """xrs_reconst_host on a host-resident batch: clean loss patterns (only
+    survivors up, written halves back) and unclean ones (repeated index, need
+    inside dpHas: whole stripes both ways), side effects included."""
+    pin = mode != "pageable"
+    if mode == "pinned_dma":
+        monkeypatch.setenv("XRS_HOST_ZC", "0")
+    stripe = 16 * size
+    if pin:
+        ptr, buf = pinned(n * stripe)
+    else:
+        buf = np.empty(n * stripe, np.uint8)
+        ptr = buf.ctypes.data
+    o = OracleXRS(D, P)
+    x = xrs_amd.XRS(D, P)
+    cases = [([0, 5], [0, 5]), ([2, 13, 15], [2, 13]), ([1, 6, 9, 12], [1, 6, 9, 12]),
+             ([3], [3, 3]), ([4, 7], [4, 8])]
+    for lost, need in cases:
+        buf[:] = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+        v = buf.reshape(n, 16, size)
+        o.encode_batch(v, size, n)
+        for j in lost:
+            v[:, j] = 0x5A
+        ref = v.copy()
+        has = [j for j in range(D + P) if j not in lost]
+        x.reconst_host(ptr, size, size, stripe, n, has, need)
+        for s in range(0, n, max(1, n // 40)):  # a sample of stripes against the oracle
+            w = [ref[s, i].copy() for i in range(D + P)]
+            o.reconst(w, has, need)
+            assert np.array_equal(v[s], np.stack(w)), (lost, need, s)
+    if pin:
+        xrs_amd.lib().xrs_host_free(ptr)

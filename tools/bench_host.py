@@ -35,16 +35,22 @@ def run(op, size, n, pinned, reps):
     buf[:] = np.random.default_rng(3).integers(0, 256, size=n * stripe, dtype=np.uint8)
     x = xrs_amd.XRS(D, P)
     x.encode_host(ptr, size, size, stripe, n)  # warm + valid stripes
+    lost2 = [0, 13]  # Reconst of one data + one piggybacked parity vect, both needed
+    has2 = [j for j in range(D + P) if j not in lost2]
     fn = ((lambda i: x.encode_host(ptr, size, size, stripe, n)) if op == "encode" else
+          (lambda i: x.reconst_host(ptr, size, size, stripe, n, has2, lost2))
+          if op == "reconst_2" else
           (lambda i: x.reconst_one_host(ptr, size, size, stripe, n, i % D)))
     fn(0)
     t0 = time.perf_counter()
     for i in range(reps):
         fn(i)
     dt = (time.perf_counter() - t0) / reps
-    algo = n * (16 if op == "encode" else 9) * size
-    h2d = n * (D if op == "encode" else 8) * size
-    d2h = n * (P if op == "encode" else 1) * size
+    # reconst_2: accounted (d + lost) * S (xrs_test.go:565); 14 survivors up,
+    # lost a-halves + needed b-halves + retrieveRS b-halves (14, 15) back
+    algo = n * {"encode": 16, "reconst_one": 9, "reconst_2": D + 2}[op] * size
+    h2d = n * {"encode": D, "reconst_one": 8, "reconst_2": D + P - 2}[op] * size
+    d2h = n * {"encode": P, "reconst_one": 1, "reconst_2": 3}[op] * size
     if pinned:
         xrs_amd.lib().xrs_host_free(ptr)
     return {"op": op, "vect_bytes": size, "stripes": n, "pinned": pinned,
@@ -81,9 +87,11 @@ def run_zero_copy(op, size, n, reps):
         fn(i)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    algo = n * (16 if op == "encode" else 9) * size
-    h2d = n * (D if op == "encode" else 8) * size
-    d2h = n * (P if op == "encode" else 1) * size
+    # reconst_2: accounted (d + lost) * S (xrs_test.go:565); 14 survivors up,
+    # lost a-halves + needed b-halves + retrieveRS b-halves (14, 15) back
+    algo = n * {"encode": 16, "reconst_one": 9, "reconst_2": D + 2}[op] * size
+    h2d = n * {"encode": D, "reconst_one": 8, "reconst_2": D + P - 2}[op] * size
+    d2h = n * {"encode": P, "reconst_one": 1, "reconst_2": 3}[op] * size
     xrs_amd.lib().xrs_host_free(ptr)
     return {"op": op, "vect_bytes": size, "stripes": n, "pinned": True, "mode": "zero-copy kernel",
             "ms": round(dt * 1e3, 3), "algorithmic_gibps": round(algo / dt / 2**30, 2),
@@ -115,8 +123,11 @@ def run_group(op, size, n, devices, reps):
 
 def main():
     cases = [("encode", 4096, 16384), ("encode", 1 << 20, 64),
-             ("reconst_one", 1 << 20, 64), ("reconst_one", 4096, 16384)]
+             ("reconst_one", 1 << 20, 64), ("reconst_one", 4096, 16384),
+             ("reconst_2", 4096, 16384), ("reconst_2", 1 << 20, 64)]
     modes = sys.argv[1:] or ["pipeline", "zero-copy"]
+    if "reconst2" in modes:  # only the general-Reconst rows, pipeline modes
+        cases, modes = [c for c in cases if c[0] == "reconst_2"], ["pipeline"]
     for op, size, n in cases:
         if "pipeline" in modes:
             for pinned, zc in ((True, "1"), (True, "0"), (False, "0")):
@@ -125,9 +136,9 @@ def main():
                 r["mode"] = "in place (zero copy)" if pinned and zc == "1" else "copy pipeline"
                 print(json.dumps(r), flush=True)
             os.environ.pop("XRS_HOST_ZC", None)
-        if "zero-copy" in modes:
+        if "zero-copy" in modes and op != "reconst_2":
             print(json.dumps(run_zero_copy(op, size, n, reps=5)), flush=True)
-        if "group" in modes:
+        if "group" in modes and op != "reconst_2":
             import torch
             ndev = torch.cuda.device_count()
             for devs in ([0], list(range(ndev))) if ndev > 1 else ([0],):

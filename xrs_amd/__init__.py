@@ -90,6 +90,7 @@ def _load():
         "xrs_replace_batched": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z, P], I),
         "xrs_encode_host": ([P, P, Z, Z, Z, Z], I),
         "xrs_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
+        "xrs_reconst_host": ([P, P, Z, Z, Z, Z, IP, I, IP, I], I),
         "xrs_host_alloc": ([Z], P),
         "xrs_host_free": ([P], None),
         "xrs_host_register": ([P, Z], I),
@@ -281,6 +282,14 @@ class XRS:
         rc = _lib.xrs_reconst_one_host(self._h, host_base, size, shard_stride, stripe_stride,
                                        n_stripes, int(k))
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else k)
+
+    def reconst_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                     n_stripes: int, dp_has, need_reconst) -> None:
+        rc = _lib.xrs_reconst_host(self._h, host_base, size, shard_stride, stripe_stride,
+                                   n_stripes, _ints(dp_has), len(dp_has), _ints(need_reconst),
+                                   len(need_reconst))
+        arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
 
     # ------------------------------------------- batched device-resident API
     # Pointers are device addresses (int); stream is a hipStream_t as int (0 = null).

@@ -1203,6 +1203,63 @@ int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, si
   });
 }
 
+// xrs.go:236 Reconst(dpHas, need) of every stripe of a host-resident batch.
+// For a clean call (indexes valid and distinct, need disjoint from dpHas)
+// only the survivors go up and only the halves the reference writes come
+// back (lost a-halves, retrieveRS b-halves of surviving piggybacked parity,
+// needed b-halves); otherwise whole stripes go both ways, so the reference's
+// toggling on repeated indexes is kept.  On an error part-way through a
+// pageable batch, earlier chunks keep their results (the reference's Reconst
+// is not atomic either).
+int xrs_reconst_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t shard_stride,
+                     size_t stripe_stride, size_t n_stripes, const int* dp_has, int n_has,
+                     const int* need, int n_need) {
+  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] >= 0 && need[0] < x->d)  // xrs.go:238-240
+    return xrs_reconst_one_host(x, host_base, size, shard_stride, stripe_stride, n_stripes,
+                                need[0]);
+  int e = check_size(size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!host_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const int d = x->d, m = x->d + x->p;
+  std::vector<int> in_has(m, 0), in_need(m, 0);
+  bool clean = n_has >= d;
+  for (int i = 0; i < n_has && clean; ++i) {
+    clean = dp_has[i] >= 0 && dp_has[i] < m && !in_has[dp_has[i]];
+    if (clean) in_has[dp_has[i]] = 1;
+  }
+  for (int u = 0; u < n_need && clean; ++u) {
+    clean = need[u] >= 0 && need[u] < m && !in_has[need[u]] && !in_need[need[u]];
+    if (clean) in_need[need[u]] = 1;
+  }
+  std::vector<std::pair<int, int>> in, out;
+  for (int i = 0; i < m; ++i) {
+    if (!clean) {
+      in.push_back({i, 2});
+      out.push_back({i, 2});
+    } else if (in_has[i]) {
+      in.push_back({i, 2});
+      if (i > d && !x->xs[i].empty()) out.push_back({i, 1});  // retrieveRS (xrs.go:305-320)
+    } else {
+      out.push_back({i, in_need[i] ? 2 : 0});
+    }
+  }
+  Written w;
+  if (uint8_t* zb = host_zero_copy(host_base, batch_extent(x, size, shard_stride, stripe_stride, n_stripes)))
+    return run_in_place(x, [&](hipStream_t s) {
+      return reconst_impl(x, {zb, shard_stride, stripe_stride}, size, n_stripes, dp_has, n_has,
+                          need, n_need, s, &w);
+    });
+  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
+  const size_t dev_stripe = static_cast<size_t>(m) * size;
+  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return reconst_impl(x, {slot, size, dev_stripe}, size, n, dp_has, n_has, need, n_need, s, &w);
+  });
+}
+
 void* xrs_host_alloc(size_t bytes) {
   void* p = nullptr;
   // Portable: pinned and mapped for every GPU, so one allocation can feed a

@@ -193,6 +193,10 @@ int xrs_group_encode_host(xrs_group *g, uint8_t *host_base, size_t size, size_t 
 int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
                                size_t shard_stride, size_t stripe_stride, size_t n_stripes,
                                int k);
+/* xrs.go:236 Reconst(dpHas, need) over a host-resident batch, split across the group. */
+int xrs_group_reconst_host(xrs_group *g, uint8_t *host_base, size_t size, size_t shard_stride,
+                           size_t stripe_stride, size_t n_stripes, const int *dp_has, int n_has,
+                           const int *need, int n_need);
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling

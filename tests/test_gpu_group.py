@@ -43,6 +43,19 @@ def test_group_host_vs_oracle(rng, devices, pinned, size, n):
     v[:, k] = 0
     g.reconst_one_host(ptr, size, size, stripe, n, k)
     assert np.array_equal(v, ref)
+    # general Reconst (one data + one piggybacked parity lost), side effects
+    # included: the stripes match the oracle's per-stripe Reconst
+    lost = [2, 14]
+    has = [j for j in range(D + P) if j not in lost]
+    v[:, lost] = 0xA5
+    exp = v.copy()
+    o = OracleXRS(D, P)
+    for s in range(n):
+        w = [exp[s, i].copy() for i in range(D + P)]
+        o.reconst(w, has, lost)
+        exp[s] = np.stack(w)
+    g.reconst_host(ptr, size, size, stripe, n, has, lost)
+    assert np.array_equal(v, exp)
     del g
     if pinned:
         xrs_amd.lib().xrs_host_free(ptr)

@@ -115,6 +115,7 @@ def _load():
         "xrs_group_codec": ([P, I], P),
         "xrs_group_encode_host": ([P, P, Z, Z, Z, Z], I),
         "xrs_group_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
+        "xrs_group_reconst_host": ([P, P, Z, Z, Z, Z, IP, I, IP, I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -375,6 +376,14 @@ class XRSGroup:
         rc = _lib.xrs_group_reconst_one_host(self._h, host_base, size, shard_stride,
                                              stripe_stride, n_stripes, int(need_reconst))
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else need_reconst)
+
+    def reconst_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
+                     n_stripes: int, dp_has, need_reconst) -> None:
+        rc = _lib.xrs_group_reconst_host(self._h, host_base, size, shard_stride, stripe_stride,
+                                         n_stripes, _ints(dp_has), len(dp_has),
+                                         _ints(need_reconst), len(need_reconst))
+        arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
+        _raise(rc, arg)
 
 
 class XRSQueue:

@@ -139,4 +139,19 @@ int xrs_group_reconst_one_host(xrs_group* g, uint8_t* host_base, size_t size, si
   });
 }
 
+// xrs.go:236 Reconst(dpHas, need) over a host-resident batch, split across
+// the group (validation and side effects: xrs_reconst_host).
+int xrs_group_reconst_host(xrs_group* g, uint8_t* host_base, size_t size, size_t shard_stride,
+                           size_t stripe_stride, size_t n_stripes, const int* dp_has, int n_has,
+                           const int* need, int n_need) {
+  if (!g) return XRS_ERR_INVALID_ARG;
+  if (size & 1) return XRS_ERR_SIZE_NOT_EVEN;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!host_base) return XRS_ERR_INVALID_ARG;
+  return for_members(g, n_stripes, [&](int i, size_t start, size_t count) {
+    return xrs_reconst_host(g->codecs[i], host_base + start * stripe_stride, size, shard_stride,
+                            stripe_stride, count, dp_has, n_has, need, n_need);
+  });
+}
+
 }  // extern "C"

@@ -166,6 +166,17 @@ int xrs_reconst_one_host(const xrs_codec *codec, uint8_t *host_base, size_t size
 int xrs_reconst_host(const xrs_codec *codec, uint8_t *host_base, size_t size, size_t shard_stride,
                      size_t stripe_stride, size_t n_stripes, const int *dp_has, int n_has,
                      const int *need, int n_need);
+/* xrs.go:324 Update over host-resident rows (layout as xrs_update_batched,
+ * host addresses; in place over PCIe when every buffer is pinned and mapped). */
+int xrs_update_host(const xrs_codec *codec, const uint8_t *old_base, size_t old_stripe_stride,
+                    const uint8_t *new_base, size_t new_stripe_stride, size_t size, int row,
+                    uint8_t *parity_base, size_t parity_shard_stride,
+                    size_t parity_stripe_stride, size_t n_stripes);
+/* xrs.go:363 Replace over host-resident rows (layout as xrs_replace_batched). */
+int xrs_replace_host(const xrs_codec *codec, const uint8_t *data_base, size_t data_shard_stride,
+                     size_t data_stripe_stride, const int *rows, int n, size_t size,
+                     uint8_t *parity_base, size_t parity_shard_stride,
+                     size_t parity_stripe_stride, size_t n_stripes);
 void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */
 void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */

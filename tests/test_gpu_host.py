@@ -135,3 +135,52 @@ def test_reconst_host_vs_oracle(rng, monkeypatch, size, n, mode):
             assert np.array_equal(v[s], np.stack(w)), (lost, need, s)
     if pin:
         xrs_amd.lib().xrs_host_free(ptr)
+
+
+@pytest.mark.parametrize("size,n", [(4096, 2000), (1026, 100), (1 << 20, 6)])
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
+def test_update_replace_host_vs_oracle(rng, monkeypatch, size, n, mode):
+    """xrs_update_host / xrs_replace_host: old, new, data and parity in
+    separate host buffers (pinned in place, pinned copy pipeline, pageable);
+    parity equals the oracle's per-stripe Update / Replace."""
+    pin = mode != "pageable"
+    if mode == "pinned_dma":
+        monkeypatch.setenv("XRS_HOST_ZC", "0")
+    allocs = []
+
+    def hbuf(nbytes):
+        if pin:
+            p_, a = pinned(nbytes)
+            allocs.append(p_)
+            return p_, a
+        a = np.empty(nbytes, np.uint8)
+        return a.ctypes.data, a
+
+    o, x = OracleXRS(D, P), xrs_amd.XRS(D, P)
+    stripe = 16 * size
+    sp, sbuf = hbuf(n * stripe)  # full stripes: data rows + parity rows
+    sbuf[:] = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+    v = sbuf.reshape(n, 16, size)
+    o.encode_batch(v, size, n)
+    np_, nbuf = hbuf(n * size)  # new data of the updated row
+    nbuf[:] = rng.integers(0, 256, size=n * size, dtype=np.uint8)
+    row = 7
+    exp = v.copy()
+    for s in range(n):
+        par = [exp[s, D + r] for r in range(P)]
+        o.update(exp[s, row].copy(), nbuf[s * size:(s + 1) * size], row, par)
+    x.update_host(sp + row * size, stripe, np_, size, size, row, sp + D * size, size, stripe, n)
+    assert np.array_equal(v, exp)
+    # Replace rows [3, 9, 0] with data from a separate buffer of 3 rows per stripe
+    rows = [3, 9, 0]
+    dp, dbuf = hbuf(n * 3 * size)
+    dbuf[:] = rng.integers(0, 256, size=n * 3 * size, dtype=np.uint8)
+    dv = dbuf.reshape(n, 3, size)
+    for s in range(n):
+        o.replace([dv[s, i] for i in range(3)], rows, [exp[s, D + r] for r in range(P)])
+    x.replace_host(dp, size, 3 * size, rows, size, sp + D * size, size, stripe, n)
+    assert np.array_equal(v, exp)
+    with pytest.raises(xrs_amd.XRSError, match="illegal data index: 12"):
+        x.update_host(sp, stripe, np_, size, size, 12, sp + D * size, size, stripe, n)
+    for p_ in allocs:
+        xrs_amd.lib().xrs_host_free(p_)

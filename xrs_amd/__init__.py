@@ -91,6 +91,8 @@ def _load():
         "xrs_encode_host": ([P, P, Z, Z, Z, Z], I),
         "xrs_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
         "xrs_reconst_host": ([P, P, Z, Z, Z, Z, IP, I, IP, I], I),
+        "xrs_update_host": ([P, P, Z, P, Z, Z, I, P, Z, Z, Z], I),
+        "xrs_replace_host": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z], I),
         "xrs_host_alloc": ([Z], P),
         "xrs_host_free": ([P], None),
         "xrs_host_register": ([P, Z], I),
@@ -291,6 +293,23 @@ class XRS:
                                    len(need_reconst))
         arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
         _raise(rc, arg)
+
+    def update_host(self, old_base: int, old_stripe_stride: int, new_base: int,
+                    new_stripe_stride: int, size: int, row: int, parity_base: int,
+                    parity_shard_stride: int, parity_stripe_stride: int, n_stripes: int) -> None:
+        rc = _lib.xrs_update_host(self._h, old_base, old_stripe_stride, new_base,
+                                  new_stripe_stride, size, int(row), parity_base,
+                                  parity_shard_stride, parity_stripe_stride, n_stripes)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
+
+    def replace_host(self, data_base: int, data_shard_stride: int, data_stripe_stride: int,
+                     replace_rows, size: int, parity_base: int, parity_shard_stride: int,
+                     parity_stripe_stride: int, n_stripes: int) -> None:
+        rc = _lib.xrs_replace_host(self._h, data_base, data_shard_stride, data_stripe_stride,
+                                   _ints(replace_rows), len(replace_rows), size, parity_base,
+                                   parity_shard_stride, parity_stripe_stride, n_stripes)
+        bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
 
     # ------------------------------------------- batched device-resident API
     # Pointers are device addresses (int); stream is a hipStream_t as int (0 = null).

@@ -770,6 +770,48 @@ int run_pipeline(const xrs_codec* x, const HostBatch& hb,
   return e ? e : es;
 }
 
+// A host row stream of a batch: stripe s of it is `len` bytes at
+// host + s * stride, staged at dev_off of the stripe's compact device slot.
+struct HostRows {
+  uint8_t* host;
+  size_t stride;
+  size_t dev_off, len;
+};
+
+// run_pipeline for operations whose rows live in separate host buffers
+// (Update: old, new and parity; Replace: data and parity): chunked H2D of
+// `in`, launch(slot, n, stream) on stripes of dev_stripe bytes, D2H of `out`.
+template <class Launch>
+int run_pipeline_rows(const xrs_codec* x, size_t n_stripes, size_t dev_stripe,
+                      const std::vector<HostRows>& in, const std::vector<HostRows>& out,
+                      Launch launch) {
+  const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
+  std::lock_guard<std::mutex> lk(x->pipe_mu);
+  DeviceGuard g(x->device);
+  int e = ensure_pipe(x, chunk * dev_stripe);
+  if (e) return e;
+  size_t i = 0;
+  for (size_t c0 = 0; c0 < n_stripes && !e; c0 += chunk, ++i) {
+    const int si = static_cast<int>(i % xrs_codec::kPipe);
+    hipStream_t st = x->pstream[si];
+    uint8_t* slot = x->slot[si];
+    const size_t nc = std::min(chunk, n_stripes - c0);
+    for (const HostRows& r : in)
+      if (!e)
+        e = copy2d(slot + r.dev_off, dev_stripe, r.host + c0 * r.stride, r.stride, r.len, nc,
+                   hipMemcpyHostToDevice, st);
+    if (!e) e = launch(slot, nc, st);
+    for (const HostRows& r : out)
+      if (!e)
+        e = copy2d(r.host + c0 * r.stride, r.stride, slot + r.dev_off, dev_stripe, r.len, nc,
+                   hipMemcpyDeviceToHost, st);
+  }
+  int es = XRS_OK;
+  for (int k = 0; k < xrs_codec::kPipe; ++k)
+    if (hipStreamSynchronize(x->pstream[k]) != hipSuccess) es = XRS_ERR_HIP;
+  return e ? e : es;
+}
+
 bool vects_ok(uint8_t* const* v, int n) {
   if (!v) return false;
   for (int i = 0; i < n; ++i)
@@ -1257,6 +1299,93 @@ int xrs_reconst_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t
   const size_t dev_stripe = static_cast<size_t>(m) * size;
   return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
     return reconst_impl(x, {slot, size, dev_stripe}, size, n, dp_has, n_has, need, n_need, s, &w);
+  });
+}
+
+// xrs.go:324 Update(old, new, row, parity) of every stripe of a host batch:
+// old/new rows at old_base / new_base + s * stride, parity shard r of stripe s
+// at parity_base + s * parity_stripe_stride + r * parity_shard_stride.
+int xrs_update_host(const xrs_codec* x, const uint8_t* old_base, size_t old_stripe_stride,
+                    const uint8_t* new_base, size_t new_stripe_stride, size_t size, int row,
+                    uint8_t* parity_base, size_t parity_shard_stride,
+                    size_t parity_stripe_stride, size_t n_stripes) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_size(size);
+  if (e) return e;
+  if (row < 0 || row >= x->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!old_base || !new_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const int p = x->p;
+  const size_t last = n_stripes - 1;
+  uint8_t* zo = host_zero_copy(const_cast<uint8_t*>(old_base), last * old_stripe_stride + size);
+  uint8_t* zn = host_zero_copy(const_cast<uint8_t*>(new_base), last * new_stripe_stride + size);
+  uint8_t* zp = host_zero_copy(parity_base, last * parity_stripe_stride +
+                                                static_cast<size_t>(p - 1) * parity_shard_stride + size);
+  if (zo && zn && zp)
+    return run_in_place(x, [&](hipStream_t s) {
+      return update_impl(x, {reinterpret_cast<uint64_t>(zo), old_stripe_stride},
+                         {reinterpret_cast<uint64_t>(zn), new_stripe_stride}, size, row,
+                         {zp, parity_shard_stride, parity_stripe_stride}, n_stripes, s);
+    });
+  // device stripe: p parity rows, then old, then new
+  const size_t dev_stripe = static_cast<size_t>(p + 2) * size;
+  std::vector<HostRows> in, out;
+  for (int r = 0; r < p; ++r) {
+    const HostRows pr{parity_base + r * parity_shard_stride, parity_stripe_stride,
+                      static_cast<size_t>(r) * size, size};
+    in.push_back(pr);
+    out.push_back(pr);
+  }
+  in.push_back({const_cast<uint8_t*>(old_base), old_stripe_stride, static_cast<size_t>(p) * size, size});
+  in.push_back({const_cast<uint8_t*>(new_base), new_stripe_stride, static_cast<size_t>(p + 1) * size, size});
+  return run_pipeline_rows(x, n_stripes, dev_stripe, in, out,
+                           [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return update_impl(x, {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p) * size), dev_stripe},
+                       {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p + 1) * size), dev_stripe},
+                       size, row, {slot, size, dev_stripe}, n, s);
+  });
+}
+
+// xrs.go:363 Replace(data, rows, parity) of every stripe of a host batch:
+// data i of stripe s at data_base + s * data_stripe_stride + i * data_shard_stride.
+int xrs_replace_host(const xrs_codec* x, const uint8_t* data_base, size_t data_shard_stride,
+                     size_t data_stripe_stride, const int* rows, int n, size_t size,
+                     uint8_t* parity_base, size_t parity_shard_stride,
+                     size_t parity_stripe_stride, size_t n_stripes) {
+  if (!x) return XRS_ERR_INVALID_ARG;
+  int e = check_replace(x, rows, n, size);
+  if (e) return e;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!data_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  if (x->device < 0) return XRS_ERR_NO_DEVICE;
+  const int p = x->p;
+  const size_t last = n_stripes - 1;
+  uint8_t* zd = host_zero_copy(const_cast<uint8_t*>(data_base),
+                               last * data_stripe_stride + static_cast<size_t>(n - 1) * data_shard_stride + size);
+  uint8_t* zp = host_zero_copy(parity_base, last * parity_stripe_stride +
+                                                static_cast<size_t>(p - 1) * parity_shard_stride + size);
+  if (zd && zp)
+    return run_in_place(x, [&](hipStream_t s) {
+      return replace_impl(x, {zd, data_shard_stride, data_stripe_stride}, rows, n, size,
+                          {zp, parity_shard_stride, parity_stripe_stride}, n_stripes, s);
+    });
+  // device stripe: p parity rows, then the n data rows
+  const size_t dev_stripe = static_cast<size_t>(p + n) * size;
+  std::vector<HostRows> in, out;
+  for (int r = 0; r < p; ++r) {
+    const HostRows pr{parity_base + r * parity_shard_stride, parity_stripe_stride,
+                      static_cast<size_t>(r) * size, size};
+    in.push_back(pr);
+    out.push_back(pr);
+  }
+  for (int i = 0; i < n; ++i)
+    in.push_back({const_cast<uint8_t*>(data_base) + i * data_shard_stride, data_stripe_stride,
+                  static_cast<size_t>(p + i) * size, size});
+  return run_pipeline_rows(x, n_stripes, dev_stripe, in, out,
+                           [&](uint8_t* slot, size_t ns, hipStream_t s) {
+    return replace_impl(x, {slot + static_cast<size_t>(p) * size, size, dev_stripe}, rows, n, size,
+                        {slot, size, dev_stripe}, ns, s);
   });
 }
 

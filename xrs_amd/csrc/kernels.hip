@@ -404,8 +404,8 @@ __global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, 
     }
   } else {
     // Runtime counts, large grid: one row at a time (measured: grouping 8
-    // loads per wave helped 4 KiB rows by 1-6% but cost 3-4% at 1 MiB;
-    // profiles/r01_bench_configs_grouped.log).
+    // loads per wave cost 0-2% at 4 KiB and 2-7% at 1 MiB over seven (d, p)
+    // in the XCD order; profiles/r01_others_rows_grouped{0,1}.log).
     for (int m = 0; m < a.nm; ++m) {
       uint32_t v[W];
       ld<VEC>(v, row_addr(a.msrc[m], stripe, off), nb);

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import xrs_amd  # noqa: E402
 
-D, P = 12, 4
+D, P = (int(v) for v in os.environ.get("CODEC", "12,4").split(","))
 ROUNDS = int(os.environ.get("ROUNDS", "11"))
 ORDERS = [None, "0", "16", "32", "64", "128", "256", "1024", "full"]
 
@@ -38,7 +38,7 @@ def main():
     staged = os.environ.get("CASES") == "staged"
     sizes = ((4096, 65536), (1 << 20, 512))
     if os.environ.get("SIZES"):  # e.g. SIZES=4128,8192: batches of ~4 GiB
-        sizes = tuple((int(v), (4 << 30) // (16 * int(v))) for v in os.environ["SIZES"].split(","))
+        sizes = tuple((int(v), (4 << 30) // ((D + P) * int(v))) for v in os.environ["SIZES"].split(","))
     if os.environ.get("CASES") == "staged":
         sizes = ((4096, 65536), (64 << 10, 4096), (1 << 20, 256), (8 << 20, 32))
     for size, n in sizes:
@@ -55,10 +55,11 @@ def main():
         shard, stripe = xrs_amd.batch_strides(size, D + P)
         buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
         base = buf.data_ptr()
-        cases.append((f"encode_{size}", 16 * size * n, buf,
+        cases.append((f"encode_{size}", (D + P) * size * n, buf,
                       lambda b=base, sz=size, sh=shard, st=stripe, nn=n:
                       x.encode_batched(b, sz, sh, st, nn, s)))
-        cases.append((f"reconst_one_{size}", 9 * size * n, buf,
+        a_need, _ = x.get_need_vects(3)
+        cases.append((f"reconst_one_{size}", ((D + 1 + len(a_need)) * size // 2 + size) * n, buf,
                       lambda b=base, sz=size, sh=shard, st=stripe, nn=n:
                       x.reconst_one_batched(b, sz, sh, st, nn, 3, s)))
     t = {(c[0], o): [] for c in cases for o in ORDERS}

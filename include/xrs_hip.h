@@ -208,6 +208,15 @@ int xrs_group_reconst_one_host(xrs_group *g, uint8_t *host_base, size_t size,
 int xrs_group_reconst_host(xrs_group *g, uint8_t *host_base, size_t size, size_t shard_stride,
                            size_t stripe_stride, size_t n_stripes, const int *dp_has, int n_has,
                            const int *need, int n_need);
+/* xrs.go:324 Update / :363 Replace over host-resident rows, split across the group. */
+int xrs_group_update_host(xrs_group *g, const uint8_t *old_base, size_t old_stripe_stride,
+                          const uint8_t *new_base, size_t new_stripe_stride, size_t size, int row,
+                          uint8_t *parity_base, size_t parity_shard_stride,
+                          size_t parity_stripe_stride, size_t n_stripes);
+int xrs_group_replace_host(xrs_group *g, const uint8_t *data_base, size_t data_shard_stride,
+                           size_t data_stripe_stride, const int *rows, int n, size_t size,
+                           uint8_t *parity_base, size_t parity_shard_stride,
+                           size_t parity_stripe_stride, size_t n_stripes);
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling

@@ -56,6 +56,21 @@ def test_group_host_vs_oracle(rng, devices, pinned, size, n):
         exp[s] = np.stack(w)
     g.reconst_host(ptr, size, size, stripe, n, has, lost)
     assert np.array_equal(v, exp)
+    # Update (row 6 <- new data) and Replace(rows 1, 10) with data in a
+    # separate buffer, parity in place
+    v[:] = ref
+    new = rng.integers(0, 256, size=(n, size), dtype=np.uint8)
+    rows = [1, 10]
+    data = rng.integers(0, 256, size=(n, 2, size), dtype=np.uint8)
+    exp = ref.copy()
+    for s in range(n):
+        par = [exp[s, D + r] for r in range(P)]
+        o.update(exp[s, 6].copy(), new[s], 6, par)
+        o.replace([data[s, 0], data[s, 1]], rows, par)
+    g.update_host(ptr + 6 * size, stripe, new.ctypes.data, size, size, 6, ptr + D * size, size,
+                  stripe, n)
+    g.replace_host(data.ctypes.data, size, 2 * size, rows, size, ptr + D * size, size, stripe, n)
+    assert np.array_equal(v, exp)
     del g
     if pinned:
         xrs_amd.lib().xrs_host_free(ptr)

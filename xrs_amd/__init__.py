@@ -118,6 +118,8 @@ def _load():
         "xrs_group_encode_host": ([P, P, Z, Z, Z, Z], I),
         "xrs_group_reconst_one_host": ([P, P, Z, Z, Z, Z, I], I),
         "xrs_group_reconst_host": ([P, P, Z, Z, Z, Z, IP, I, IP, I], I),
+        "xrs_group_update_host": ([P, P, Z, P, Z, Z, I, P, Z, Z, Z], I),
+        "xrs_group_replace_host": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -395,6 +397,24 @@ class XRSGroup:
         rc = _lib.xrs_group_reconst_one_host(self._h, host_base, size, shard_stride,
                                              stripe_stride, n_stripes, int(need_reconst))
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else need_reconst)
+
+    def update_host(self, old_base: int, old_stripe_stride: int, new_base: int,
+                    new_stripe_stride: int, size: int, row: int, parity_base: int,
+                    parity_shard_stride: int, parity_stripe_stride: int, n_stripes: int) -> None:
+        rc = _lib.xrs_group_update_host(self._h, old_base, old_stripe_stride, new_base,
+                                        new_stripe_stride, size, int(row), parity_base,
+                                        parity_shard_stride, parity_stripe_stride, n_stripes)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
+
+    def replace_host(self, data_base: int, data_shard_stride: int, data_stripe_stride: int,
+                     replace_rows, size: int, parity_base: int, parity_shard_stride: int,
+                     parity_stripe_stride: int, n_stripes: int) -> None:
+        rc = _lib.xrs_group_replace_host(self._h, data_base, data_shard_stride,
+                                         data_stripe_stride, _ints(replace_rows),
+                                         len(replace_rows), size, parity_base,
+                                         parity_shard_stride, parity_stripe_stride, n_stripes)
+        bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
+        _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else bad)
 
     def reconst_host(self, host_base: int, size: int, shard_stride: int, stripe_stride: int,
                      n_stripes: int, dp_has, need_reconst) -> None:

@@ -154,4 +154,43 @@ int xrs_group_reconst_host(xrs_group* g, uint8_t* host_base, size_t size, size_t
   });
 }
 
+// xrs.go:324 Update over host-resident rows, split across the group.
+int xrs_group_update_host(xrs_group* g, const uint8_t* old_base, size_t old_stripe_stride,
+                          const uint8_t* new_base, size_t new_stripe_stride, size_t size, int row,
+                          uint8_t* parity_base, size_t parity_shard_stride,
+                          size_t parity_stripe_stride, size_t n_stripes) {
+  if (!g) return XRS_ERR_INVALID_ARG;
+  if (size & 1) return XRS_ERR_SIZE_NOT_EVEN;
+  if (row < 0 || row >= xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!old_base || !new_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  return for_members(g, n_stripes, [&](int i, size_t start, size_t count) {
+    return xrs_update_host(g->codecs[i], old_base + start * old_stripe_stride, old_stripe_stride,
+                           new_base + start * new_stripe_stride, new_stripe_stride, size, row,
+                           parity_base + start * parity_stripe_stride, parity_shard_stride,
+                           parity_stripe_stride, count);
+  });
+}
+
+// xrs.go:363 Replace over host-resident rows, split across the group.
+int xrs_group_replace_host(xrs_group* g, const uint8_t* data_base, size_t data_shard_stride,
+                           size_t data_stripe_stride, const int* rows, int n, size_t size,
+                           uint8_t* parity_base, size_t parity_shard_stride,
+                           size_t parity_stripe_stride, size_t n_stripes) {
+  if (!g) return XRS_ERR_INVALID_ARG;
+  if (n < 1 || n > xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_VECTS;
+  if (size & 1) return XRS_ERR_SIZE_NOT_EVEN;
+  if (!rows) return XRS_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_DATA_INDEX;
+  if (n_stripes == 0 || size == 0) return XRS_OK;
+  if (!data_base || !parity_base) return XRS_ERR_INVALID_ARG;
+  return for_members(g, n_stripes, [&](int i, size_t start, size_t count) {
+    return xrs_replace_host(g->codecs[i], data_base + start * data_stripe_stride,
+                            data_shard_stride, data_stripe_stride, rows, n, size,
+                            parity_base + start * parity_stripe_stride, parity_shard_stride,
+                            parity_stripe_stride, count);
+  });
+}
+
 }  // extern "C"

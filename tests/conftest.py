@@ -9,6 +9,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "xrs_golden.npz")
+GOLDEN_CODECS = os.path.join(ROOT, "tests", "golden", "xrs_golden_codecs.npz")
 
 
 def pytest_configure(config):
@@ -19,6 +20,12 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def golden_codecs():
+    with np.load(GOLDEN_CODECS, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
 
 

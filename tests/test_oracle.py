@@ -252,3 +252,25 @@ def test_cpu_baseline_batch_paths(monkeypatch, level, d, p):
         host[:, k] = 0x5A
         o.reconst_one_batch(host, size, n, k, threads)
         assert np.array_equal(host, ref), (level, size, k)
+
+
+@pytest.mark.parametrize("cls", ORACLES)
+@pytest.mark.parametrize("S", [34, 2048])
+@pytest.mark.parametrize("d,p", [(10, 4), (6, 3), (5, 5), (4, 2), (20, 4), (1, 2), (30, 6)])
+def test_golden_codecs(golden_codecs, cls, d, p, S):
+    """Both restatements reproduce the committed goldens of the other codecs
+    (tests/golden/make_golden_codecs.py): Encode, Reconst, Update, Replace."""
+    g, k, x = golden_codecs, f"d{d}p{p}_S{S}_", cls(d, p)
+    v = [r.copy() for r in g[k + "enc_in"]] + [np.zeros(S, np.uint8) for _ in range(p)]
+    x.encode(v)
+    assert np.array_equal(np.stack(v), g[k + "enc_out"])
+    for i in range(2):
+        v = [r.copy() for r in g[k + f"rc{i}_in"]]
+        x.reconst(v, list(g[k + f"rc{i}_has"]), list(g[k + f"rc{i}_need"]))
+        assert np.array_equal(np.stack(v), g[k + f"rc{i}_out"]), i
+    par = [r.copy() for r in g[k + "up_in"]]
+    x.update(g[k + "up_old"].copy(), g[k + "up_new"].copy(), int(g[k + "up_row"][0]), par)
+    assert np.array_equal(np.stack(par), g[k + "up_out"])
+    par = [r.copy() for r in g[k + "rp_in"]]
+    x.replace([r.copy() for r in g[k + "rp_data"]], list(g[k + "rp_rows"]), par)
+    assert np.array_equal(np.stack(par), g[k + "rp_out"])

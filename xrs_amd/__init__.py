@@ -20,7 +20,8 @@ import threading
 __all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libxrs_hip.so")
+# XRS_LIB: an alternative build of the library (A/B experiments only).
+LIB_PATH = os.environ.get("XRS_LIB") or os.path.join(_HERE, "libxrs_hip.so")
 
 XRS_ERR_SIZE_NOT_EVEN = -2
 XRS_ERR_ILLEGAL_DATA_INDEX = -3

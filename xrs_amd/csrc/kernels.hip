@@ -32,7 +32,10 @@ namespace xrs {
 namespace {
 
 constexpr int kDyn = -1;  // count known only at run time
-constexpr int kBlock = 256;
+#ifndef XRS_BLOCK
+#define XRS_BLOCK 256  // threads per block (-DXRS_BLOCK=... for A/B builds only)
+#endif
+constexpr int kBlock = XRS_BLOCK;
 constexpr uint64_t kMaxBlocks = 0x7fffffffu;  // 1-D grid limit
 constexpr uint64_t kLatencyGrid = 256;         // blocks: one per CU (MI355X: 256 CUs)
 
@@ -207,10 +210,10 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
   }
 }
 
-template <int P, int C, bool ACC, bool VEC>
-__global__ __launch_bounds__(kBlock) void pair_kernel(const PairArgs<P, C, VEC> a) {
+template <int P, int C, bool ACC, bool VEC, int BS = kBlock>
+__global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
@@ -343,10 +346,10 @@ __device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, c
   }
 }
 
-template <int R, int NM, int NX, bool ACC, bool VEC>
-__global__ __launch_bounds__(kBlock) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
+template <int R, int NM, int NX, bool ACC, bool VEC, int BS = kBlock>
+__global__ __launch_bounds__(BS) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
@@ -678,7 +681,7 @@ enum class Shape { kPair, kRows, kStaged };
 //    (profiles/r01_order_sweep_staged.log).
 // The byte-granular (!VEC) path keeps the plain order.  XRS_BLOCK_ORDER=<K>
 // overrides (0: plain order; "full": one range per XCD) for A/B runs.
-BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
+BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks, int bs = kBlock) {
   BlockOrder o{static_cast<uint32_t>(blocks), 0};
   if (!vec) return o;
   if (const char* e = std::getenv("XRS_BLOCK_ORDER")) {
@@ -694,11 +697,24 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks) {
       else if (len < (1u << 20)) o.k = 128;
       break;  // half >= 1 MiB: plain order
     case Shape::kRows:
+      if (bs == 1024 && len >= (256u << 10)) {  // 16 KiB blocks: K = half / 4 KiB, <= 256
+        o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 12));
+        break;
+      }
       if (len <= 4096) o.k = static_cast<uint32_t>(blocks / 8);
       else if (len >= (256u << 10)) o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 13));
       break;
   }
   return o;
+}
+
+// Threads per block for a kernel family: `def`, or the env override when it
+// names a size this build instantiates for that family.
+int env_block(const char* var, int def) {
+  const char* e = std::getenv(var);
+  if (!e || !*e) return def;
+  const int v = std::atoi(e);
+  return (v == 256 || v == def) ? v : def;
 }
 
 template <int NL, int NN, bool VEC>
@@ -840,10 +856,24 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
-  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  // 128-thread blocks for the 16-byte kernels on halves up to 4 KiB (Encode
+  // at 4 KiB +1-2.5% over 256; at 1 MiB -1.5..+0.9%, so 256 stays there:
+  // profiles/r01_blocksize.log).  XRS_PAIR_BLOCK=256 / 128 forces either.
+  const char* pb = std::getenv("XRS_PAIR_BLOCK");
+  const int bs = !VEC ? kBlock
+                      : (pb && *pb) ? env_block("XRS_PAIR_BLOCK", 128)
+                                    : (p.half <= 4096 ? 128 : kBlock);
+  const uint64_t blocks = (a.total + bs - 1) / bs;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
-  a.order = block_order(Shape::kPair, VEC, p.half, blocks);
+  a.order = block_order(Shape::kPair, VEC, p.half, blocks, bs);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  if constexpr (VEC) {
+    if (bs == 128) {
+      hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC, 128>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(128), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());
@@ -889,13 +919,23 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
-  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  // 1024-thread blocks for rows of >= 256 KiB (ReconstOne at 1 MiB vects:
+  // +3-5% over 256, profiles/r01_blocksize.log); XRS_ROWS_BLOCK=256 for A/B.
+  const int bs = (VEC && p.len >= (256u << 10)) ? env_block("XRS_ROWS_BLOCK", 1024) : kBlock;
+  const uint64_t blocks = (a.total + bs - 1) / bs;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
-  a.order = block_order(Shape::kRows, VEC, p.len, blocks);
+  a.order = block_order(Shape::kRows, VEC, p.len, blocks, bs);
   // XRS_ROWS_GROUPED=0 / =1 forces either runtime-count loop (A/B, tests).
   const char* gv = std::getenv("XRS_ROWS_GROUPED");
-  a.grouped = (gv && *gv) ? gv[0] != '0' : blocks < kLatencyGrid;
+  a.grouped = (gv && *gv) ? gv[0] != '0' : blocks * bs < kLatencyGrid * kBlock;
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  if constexpr (VEC) {
+    if (bs == 1024) {
+      hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC, 1024>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(1024), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());

@@ -190,17 +190,17 @@ def main():
     # The four timed launches of a step, in order: (key, kernel, algorithmic
     # bytes per launch, read bytes per launch, launcher).
     launches = [
-        ("encode_4k", "pair_kernel<4,12,false,true>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
+        ("encode_4k", "pair_kernel<4,12,false,true,128>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
          lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
                                     stream)),
-        ("reconst_one_4k", "rows_kernel<2,12,4,false,true>", n_enc * 9 * ENC_S,
+        ("reconst_one_4k", "rows_kernel<2,12,4,false,true,256>", n_enc * 9 * ENC_S,
          n_enc * 8 * ENC_S,
          lambda i: x.reconst_one_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
                                          i % D, stream)),
-        ("encode_1m", "pair_kernel<4,12,false,true>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
+        ("encode_1m", "pair_kernel<4,12,false,true,256>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
          lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
                                     stream)),
-        ("reconst_one_1m", "rows_kernel<2,12,4,false,true>", n_rec * 9 * REC_S,
+        ("reconst_one_1m", "rows_kernel<2,12,4,false,true,1024>", n_rec * 9 * REC_S,
          n_rec * 8 * REC_S,
          lambda i: x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
                                          i % D, stream)),

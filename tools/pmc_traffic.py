@@ -22,10 +22,10 @@ from collections import defaultdict
 
 # bench.py kernel keys -> (kernel-name fragment, grid threads of the timed launch)
 KERNELS = {
-    "encode_4k": ("pair_kernel<4, 12, false, true>", 65536 * 128),
-    "reconst_one_4k": ("rows_kernel<2, 12, 4, false, true>", 65536 * 128),
-    "encode_1m": ("pair_kernel<4, 12, false, true>", 512 * 32768),
-    "reconst_one_1m": ("rows_kernel<2, 12, 4, false, true>", 512 * 32768),
+    "encode_4k": ("pair_kernel<4, 12, false, true, 128>", 65536 * 128),
+    "reconst_one_4k": ("rows_kernel<2, 12, 4, false, true, 256>", 65536 * 128),
+    "encode_1m": ("pair_kernel<4, 12, false, true, 256>", 512 * 32768),
+    "reconst_one_1m": ("rows_kernel<2, 12, 4, false, true, 1024>", 512 * 32768),
 }
 ALGO_BYTES = {"encode_4k": 65536 * 16 * 4096, "reconst_one_4k": 65536 * 9 * 4096,
               "encode_1m": 512 * 16 * (1 << 20), "reconst_one_1m": 512 * 9 * (1 << 20)}

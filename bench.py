@@ -17,33 +17,57 @@ of the four (operation, vect size) pairs the north star names:
 ReconstOne rebuilds data shard k = step mod 12.
 value = algorithmic bytes of all ranks / max-over-ranks time, in GiB/s.  Inputs
 are synthetic, generated on the device, and resident in HBM before timing.
-Multi-GPU: one process per GPU, each with its own batch (weak scaling, no
-collective on the data path; the barrier and the max-time all-reduce only
-bracket the timed region).
+
+Multi-GPU (xrs_amd/dist.py): one process per GPU.  Under torchrun the ranks
+come from WORLD_SIZE (which must equal --gpus); `python bench.py --gpus N`
+without a launcher starts the N rank processes itself before any GPU call.
+Each rank owns its own batch (weak scaling, no collective on the data path;
+the barrier and the per-rank time gather only bracket the timed regions).
+
+After the headline timed region, the same line carries:
+  * "config5": BASELINE config 5, Encode + ReconstOne of --config5-stripes
+    stripes of 1 MiB vects per rank (8,192 = 128 GiB resident per GPU; at
+    N = 8 the 65,536-stripe, 1 TiB batch split 8 ways), with its own
+    per-rank times;
+  * "host_e2e": the host-resident path (shards start and end in pinned host
+    memory, xrs_*_host, PCIe-inclusive) on every rank at once;
+  * "xgmi_repair" (N >= 2, two visible GPUs): rank 0 rebuilds a data shard
+    with half of its need set on the peer GPU (xGMI reads), checked bit for
+    bit against the same rebuild from local shards.
 
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import importlib.util
 import json
 import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import xrs_amd  # noqa: E402
+
+def _load_dist():
+    """xrs_amd/dist.py without the package __init__ (which loads the HIP
+    library): the parent of a self-launched run must not touch the GPU."""
+    spec = importlib.util.spec_from_file_location("xrs_bench_dist",
+                                                  os.path.join(ROOT, "xrs_amd", "dist.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+xdist = _load_dist()
 
 D, P = 12, 4
 ENC_S = 4096
 REC_S = 1 << 20
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
 
 
 def log(*a):
@@ -64,6 +88,8 @@ def _cpu_model() -> str:
 def _cpu_rates(o, seconds: float, threads: int):
     """Bytes/s of the oracle's batch path on `threads` for the four bench
     kernels, each run for seconds/4 on a bounded sample."""
+    import numpy as np
+
     rng = np.random.Generator(np.random.PCG64(1))
 
     def run(fn, nbytes):
@@ -97,7 +123,7 @@ def cpu_baseline(seconds: float, step_bytes: dict):
 
     def mix(rates):  # same byte mix as one GPU step
         t_step = sum(step_bytes[k] / rates[k] for k in step_bytes)
-        return sum(step_bytes.values()) / t_step / 2**30
+        return sum(step_bytes.values()) / t_step / GIB
 
     r1 = _cpu_rates(o, seconds, 1)
     try:
@@ -110,9 +136,9 @@ def cpu_baseline(seconds: float, step_bytes: dict):
         "value": round(mix(r1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
         "simd": ("scalar", "avx2", "avx512bw")[lib().oxrs_simd_level()],
         "cpu_model": _cpu_model(),
-        "gibps": {k: round(v / 2**30, 3) for k, v in r1.items()},
+        "gibps": {k: round(v / GIB, 3) for k, v in r1.items()},
         "multi_thread": {"threads": threads, "value": round(mix(rn), 3),
-                         "gibps": {k: round(v / 2**30, 3) for k, v in rn.items()}},
+                         "gibps": {k: round(v / GIB, 3) for k, v in rn.items()}},
         "sample": (f"oracle/xrs_oracle.c: Encode and ReconstOne of 16384 12+4 stripes @ 4 KiB "
                    f"(1 GiB) and of 64 stripes @ 1 MiB (1 GiB), each repeated for "
                    f"{seconds / 4:.1f} s on 1 thread and {seconds / 8:.1f} s on {threads} "
@@ -131,150 +157,344 @@ def pmc_traffic(kernel_key: str):
         return None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--enc-stripes", type=int, default=65536)
     ap.add_argument("--rec-stripes", type=int, default=512)
+    ap.add_argument("--config5-stripes", type=int, default=8192,
+                    help="1 MiB stripes per rank for the config5 key (0: skip)")
+    ap.add_argument("--config5-steps", type=int, default=5)
+    ap.add_argument("--host-mib", type=int, default=1024,
+                    help="MiB per host-resident batch for the host_e2e key (0: skip)")
+    ap.add_argument("--xgmi-stripes", type=int, default=64,
+                    help="1 MiB stripes for the xgmi_repair key (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--ramp-seconds", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    # One process per GPU.  XRS_DIST_BACKEND=gloo rehearses N ranks on fewer
-    # GPUs (ranks share a card); the driver's runs use nccl (RCCL), one per GPU.
-    backend = os.environ.get("XRS_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    torch.cuda.set_device(local % ndev)
-    dev = torch.device("cuda", local % ndev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
+class Rank:
+    """Per-rank state: device, stream, codec and the timing bracket."""
 
-    x = xrs_amd.XRS(D, P)
-    stream = torch.cuda.current_stream().cuda_stream
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + rank)
+    def __init__(self, w, backend: str):
+        import torch
+
+        import xrs_amd
+
+        self.torch, self.xrs_amd, self.w = torch, xrs_amd, w
+        self.ndev = torch.cuda.device_count()
+        if self.ndev < 1:
+            raise RuntimeError("bench.py needs a GPU (there is no CPU fallback)")
+        self.dev_index = w.local % self.ndev
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+        xdist.init(w, backend, self.dev)
+        # the time gather runs on the device for RCCL, on the host for gloo
+        self.tdev = self.dev if (w.world > 1 and backend == "nccl") else None
+        self.x = xrs_amd.XRS(D, P)
+        self.stream = torch.cuda.current_stream().cuda_stream
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def timed(self, step, steps, warmup):
+        return xdist.timed_steps(step, steps, warmup, self.sync, self.tdev)
+
+    def random_bytes(self, n: int, seed: int):
+        """n uniform random bytes on the device, filled 1 GiB at a time."""
+        torch = self.torch
+        buf = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(seed)
+        step = 1 << 30
+        for a in range(0, n, step):
+            buf[a:a + step].random_(0, 256, generator=g)
+        return buf
+
+    def ramp(self, fn, seconds: float):
+        """Clock ramp (untimed): an idle MI355X runs its first ~50 launches of
+        this size up to 30% slower (tools/first_alloc_probe.py,
+        profiles/r01_first_alloc.log)."""
+        t = time.perf_counter()
+        while time.perf_counter() - t < seconds:
+            fn()
+            self.sync()
+
+
+def headline(R: Rank, args):
+    """The metric's timed region: the four launches of one step."""
+    torch, x, s = R.torch, R.x, R.stream
     n_enc, n_rec = args.enc_stripes, args.rec_stripes
     # Device batch layout: the library's recommended strides (xrs_batch_strides):
     # shards back to back at 4 KiB and 1 MiB (the kernels' XCD-aware block
     # order makes padding unnecessary below 4 MiB).
-    enc_shard, enc_stripe = xrs_amd.batch_strides(ENC_S, D + P)
-    rec_shard, rec_stripe = xrs_amd.batch_strides(REC_S, D + P)
-    enc_buf = torch.randint(0, 256, (n_enc * enc_stripe,), dtype=torch.uint8, device=dev,
-                            generator=g)
-    rec_buf = torch.randint(0, 256, (n_rec * rec_stripe,), dtype=torch.uint8, device=dev,
-                            generator=g)
-    x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
-    x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, stream)
-    torch.cuda.synchronize()
-    # Clock ramp (setup, untimed): an idle MI355X runs its first ~50 launches
-    # of this size up to 30% slower (tools/first_alloc_probe.py,
-    # profiles/r01_first_alloc.log).  Repeat the (idempotent) setup encode for
-    # --ramp-seconds before the W warmup steps.
-    t_ramp = time.perf_counter()
-    while time.perf_counter() - t_ramp < args.ramp_seconds:
-        x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, stream)
-        torch.cuda.synchronize()
+    enc_shard, enc_stripe = R.xrs_amd.batch_strides(ENC_S, D + P)
+    rec_shard, rec_stripe = R.xrs_amd.batch_strides(REC_S, D + P)
+    first_enc = xdist.stripe_range(n_enc * R.w.world, R.w.rank, R.w.world)[0]
+    enc_buf = R.random_bytes(n_enc * enc_stripe, 0x5EED + first_enc)
+    rec_buf = R.random_bytes(n_rec * rec_stripe, 0xB1D + first_enc)
+    x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s)
+    x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, s)
+    R.sync()
+    R.ramp(lambda: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s),
+           args.ramp_seconds)
     # The four timed launches of a step, in order: (key, kernel, algorithmic
     # bytes per launch, read bytes per launch, launcher).
     launches = [
         ("encode_4k", "pair_kernel<4,12,false,true,128>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
-         lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
-                                    stream)),
+         lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s)),
         ("reconst_one_4k", "rows_kernel<2,12,4,false,true,256>", n_enc * 9 * ENC_S,
          n_enc * 8 * ENC_S,
          lambda i: x.reconst_one_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
-                                         i % D, stream)),
+                                         i % D, s)),
         ("encode_1m", "pair_kernel<4,12,false,true,256>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
-         lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
-                                    stream)),
+         lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, s)),
         ("reconst_one_1m", "rows_kernel<2,12,4,false,true,1024>", n_rec * 9 * REC_S,
          n_rec * 8 * REC_S,
          lambda i: x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
-                                         i % D, stream)),
+                                         i % D, s)),
     ]
     launches = [l for l in launches if l[2] > 0]
     step_bytes = sum(l[2] for l in launches)
     nl = len(launches)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(nl + 1)] for _ in range(args.steps)]
+    state = {"timed": False, "i": 0}
 
-    def step(i, events=None):
+    def step(i):
+        events = ev[state["i"]] if state["timed"] else None
         for j, l in enumerate(launches):
             if events:
                 events[j].record()
             l[4](i)
         if events:
             events[nl].record()
+            state["i"] += 1
 
+    # warmup steps untimed, then exactly args.steps timed ones (with events)
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, ev[i])
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    barrier()
-    # Every rank's time (one slot each, summed), so the max and the spread
-    # across ranks are both reported.
-    t = torch.zeros(world, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    t[rank] = elapsed
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    rank_seconds = [float(v) for v in t.cpu()]
-    elapsed_max = max(rank_seconds)
-    total_bytes = world * args.steps * step_bytes
-    value = total_bytes / elapsed_max / 2**30
+    state["timed"] = True
+    rank_seconds = R.timed(step, args.steps, 0)
 
     kernels = {}
     for j, (key, kname, nbytes, rbytes, _) in enumerate(launches):
-        ms = float(np.mean([e[j].elapsed_time(e[j + 1]) for e in ev]))
+        ms = sum(e[j].elapsed_time(e[j + 1]) for e in ev) / len(ev)
         kernels[key] = {
             "kernel": kname, "ms": round(ms, 4), "bytes_per_launch": nbytes,
-            "gibps": round(nbytes / (ms / 1e3) / 2**30, 1),
+            "gibps": round(nbytes / (ms / 1e3) / GIB, 1),
             "achieved_gbs": round(nbytes / (ms / 1e3) / 1e9, 1),
             "frac": round(nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "read_only_gbs": round(rbytes / (ms / 1e3) / 1e9, 1),
+            "read_frac": round(rbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+    del enc_buf, rec_buf
+    torch.cuda.empty_cache()
+    return launches, step_bytes, rank_seconds, kernels, (enc_shard, rec_shard)
+
+
+def config5(R: Rank, args):
+    """BASELINE config 5: Encode and ReconstOne of 1 MiB stripes, a fixed
+    number per rank (8,192 = 128 GiB per GPU; 65,536 stripes = 1 TiB over 8),
+    split by xdist.stripe_range; no collective.  Reference workload:
+    xrs_test.go:476-480 (1 MiB Encode), xrs.go:175-221 (ReconstOne)."""
+    torch, x, s = R.torch, R.x, R.stream
+    w = R.w
+    total = args.config5_stripes * w.world
+    first, n = xdist.stripe_range(total, w.rank, w.world)
+    shard, stripe = R.xrs_amd.batch_strides(REC_S, D + P)
+    t0 = time.perf_counter()
+    buf = R.random_bytes(n * stripe, 0xC05 + first)
+    base = buf.data_ptr()
+    x.encode_batched(base, REC_S, shard, stripe, n, s)
+    R.sync()
+    log(f"rank {w.rank}: config5 batch of {n} stripes ({n * stripe / GIB:.1f} GiB) ready in "
+        f"{time.perf_counter() - t0:.1f} s")
+    R.ramp(lambda: x.encode_batched(base, REC_S, shard, stripe, n, s), 0.2)
+    enc_sec = R.timed(lambda i: x.encode_batched(base, REC_S, shard, stripe, n, s),
+                      args.config5_steps, 1)
+    rec_sec = R.timed(lambda i: x.reconst_one_batched(base, REC_S, shard, stripe, n, i % D, s),
+                      args.config5_steps, 1)
+    # Round trip on a sample (no oracle on the product path): erase shard k of
+    # the first stripes, rebuild the whole batch, compare with the saved bytes.
+    k, m = 7, min(n, 64)
+    view = buf.view(n, stripe)[:m, k * shard:k * shard + REC_S]
+    saved = view.clone()
+    view.zero_()
+    x.reconst_one_batched(base, REC_S, shard, stripe, n, k, s)
+    R.sync()
+    ok = bool(torch.equal(view, saved))
+    del buf, view, saved
+    torch.cuda.empty_cache()
+    enc_bytes, rec_bytes = n * (D + P) * REC_S, n * 9 * REC_S
+    steps = args.config5_steps
+    enc_t, rec_t = max(enc_sec), max(rec_sec)
+    world_bytes = lambda per: per * w.world  # every rank holds the same count (+-1 stripe)
+    return {
+        "workload": (f"12+4 @ 1 MiB: {total} stripes ({total * (D + P) * REC_S / 2**40:.3f} TiB) "
+                     f"split {n} per GPU over {w.world} GPU(s), no collective"),
+        "stripes_total": total, "stripes_per_rank": n,
+        "steps": steps,
+        "encode": {"rank_seconds": [round(v, 6) for v in enc_sec],
+                   "gibps": round(world_bytes(enc_bytes) * steps / enc_t / GIB, 1),
+                   "frac_per_gpu": round(enc_bytes * steps / enc_t / 1e9 / HBM_PEAK_GBS, 4)},
+        "reconst_one": {"rank_seconds": [round(v, 6) for v in rec_sec],
+                        "gibps": round(world_bytes(rec_bytes) * steps / rec_t / GIB, 1),
+                        "frac_per_gpu": round(rec_bytes * steps / rec_t / 1e9 / HBM_PEAK_GBS, 4)},
+        "gibps": round(world_bytes(enc_bytes + rec_bytes) * steps / (enc_t + rec_t) / GIB, 1),
+        "roundtrip_ok_rank0": ok,
+    }, ok
+
+
+def host_e2e(R: Rank, args):
+    """Shards start and end in host memory: pinned, device-mapped batches
+    (xrs_host_alloc) run in place over PCIe by xrs_encode_host /
+    xrs_reconst_one_host, every rank at once over its own link.  Reference
+    call sites: xrs.go:103-128 (Encode), :175-221 (ReconstOne)."""
+    import ctypes
+
+    import numpy as np
+
+    torch, x, L = R.torch, R.x, R.xrs_amd.lib()
+    out = {}
+    for key, size, kind in (("encode_4k", ENC_S, "enc"), ("reconst_one_1m", REC_S, "rec")):
+        stripe = (D + P) * size
+        n = max(1, (args.host_mib << 20) // stripe)
+        nbytes = n * stripe
+        ptr = L.xrs_host_alloc(nbytes)
+        if not ptr:
+            raise RuntimeError("xrs_host_alloc failed")
+        try:
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
+            torch.from_numpy(host).copy_(R.random_bytes(nbytes, 0x4057 + R.w.rank))
+            x.encode_host(ptr, size, size, stripe, n)
+            if kind == "enc":
+                fn = lambda i: x.encode_host(ptr, size, size, stripe, n)
+                algo = n * (D + P) * size
+            else:
+                fn = lambda i: x.reconst_one_host(ptr, size, size, stripe, n, i % D)
+                algo = n * 9 * size
+            fn(0)
+            secs = R.timed(fn, 3, 1)
+            out[key] = {"stripes_per_rank": n, "bytes_per_call": algo,
+                        "rank_gibps": [round(algo * 3 / t / GIB, 2) for t in secs],
+                        "gibps": round(algo * 3 * R.w.world / max(secs) / GIB, 2)}
+        finally:
+            L.xrs_host_free(ptr)
+    out["path"] = "pinned host memory, kernels in place over PCIe (xrs_*_host zero-copy)"
+    return out
+
+
+def xgmi_repair(R: Rank, args):
+    """Cross-GPU repair: rank 0 rebuilds data shard k of
+    1 MiB stripes whose odd-numbered shards live on the peer GPU, reading them
+    over xGMI (xrs_reconst_one_shards after xrs_enable_peer_access), and checks
+    the result bit for bit against the rebuild from all-local shards.
+    Semantics: xrs.go:175-221."""
+    torch, x, s = R.torch, R.x, R.stream
+    if R.ndev < 2:
+        return {"skipped": f"{R.ndev} GPU visible to rank 0"}
+    peer = (R.dev_index + 1) % R.ndev
+    rc = R.xrs_amd.lib().xrs_enable_peer_access(R.dev_index, peer)
+    if rc != 0:
+        return {"skipped": f"peer access {R.dev_index}->{peer} unavailable (code {rc})"}
+    n, size, k = args.xgmi_stripes, REC_S, 4
+    col = n * size  # shard-major: shard i of stripe t at base + i*col + t*size
+    local = R.random_bytes((D + P) * col, 0x961)
+    x.encode_batched(local.data_ptr(), size, col, size, n, s)
+    R.sync()
+    expect = local[k * col:(k + 1) * col].clone()
+    remote = {i: local[i * col:(i + 1) * col].to(f"cuda:{peer}") for i in range(1, D + P, 2)}
+    torch.cuda.synchronize(peer)
+
+    def table():
+        return [remote[i].data_ptr() if i in remote else local.data_ptr() + i * col
+                for i in range(D + P)]
+
+    tab = table()
+    a_need, b_need = x.get_need_vects(k)
+    need = sorted(set([m for m in range(D) if m != k] + b_need + a_need))
+    on_peer = sum(1 for i in need if i in remote)
+    local[k * col:(k + 1) * col].zero_()
+    x.reconst_one_shards(tab, size, size, n, k, s)
+    R.sync()
+    exact = bool(torch.equal(local[k * col:(k + 1) * col], expect))
+    # same rebuild from all-local shards, for the rate next to it
+    lt = [local.data_ptr() + i * col for i in range(D + P)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rates = {}
+    for name, t in (("mixed", tab), ("local", lt)):
+        for _ in range(2):
+            x.reconst_one_shards(t, size, size, n, k, s)
+        reps = 10
+        e0.record()
+        for _ in range(reps):
+            x.reconst_one_shards(t, size, size, n, k, s)
+        e1.record()
+        R.sync()
+        ms = e0.elapsed_time(e1) / reps
+        rates[name] = round(n * 9 * size / (ms / 1e3) / 1e9, 1)
+    exact = exact and bool(torch.equal(local[k * col:(k + 1) * col], expect))
+    del remote, local, expect
+    torch.cuda.empty_cache()
+    return {"device": R.dev_index, "peer": peer, "stripes": n, "vect_bytes": size, "k": k,
+            "need_halves_on_peer": f"{on_peer} of {len(need)} need-set shards",
+            "xgmi_bitexact": exact,
+            "gbs_algorithmic": rates["mixed"], "gbs_all_local": rates["local"],
+            "bytes_per_call": n * 9 * size}
+
+
+def run_rank(args, w):
+    backend = os.environ.get("XRS_DIST_BACKEND", "nccl")
+    R = Rank(w, backend)
+    launches, step_bytes, rank_seconds, kernels, strides = headline(R, args)
+    elapsed_max = max(rank_seconds)
+    value = w.world * args.steps * step_bytes / elapsed_max / GIB
+
     dom_key = max(kernels, key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_key]
-    traffic = pmc_traffic(dom_key)
     roofline = {
         "bound": "hbm", "kernel": dom["kernel"], "launch": dom_key,
         "achieved": dom["achieved_gbs"],
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom["achieved_gbs"] / HBM_PEAK_GBS, 4),
-        "traffic": traffic,
+        "traffic": pmc_traffic(dom_key),
         "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
-        # the north star's "HBM-read roofline": read bytes only over the same peak
+        # the north star's "HBM-read roofline": read bytes only over the same
+        # peak (DESIGN.md §5 explains why 0.70 of it is out of reach for a
+        # 12:4 read:write pattern)
         "read_achieved": dom["read_only_gbs"],
-        "read_frac": round(dom["read_only_gbs"] / HBM_PEAK_GBS, 4),
+        "read_frac": dom["read_frac"],
     }
 
+    c5 = None
+    if args.config5_stripes > 0:
+        c5, _ = config5(R, args)
+    he = host_e2e(R, args) if args.host_mib > 0 else None
+    xg = None
+    if w.world > 1 and args.xgmi_stripes > 0:
+        xdist.barrier()
+        if w.rank == 0:
+            xg = xgmi_repair(R, args)
+        xdist.barrier()
+    elif args.xgmi_stripes > 0:
+        xg = {"skipped": "N = 1 (cross-GPU repair runs at N >= 2)"}
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if w.rank == 0 and w.world == 1 and not args.no_cpu_baseline:
         log("timing CPU baseline ...")
         cpu = cpu_baseline(args.cpu_seconds, {l[0]: l[2] for l in launches})
 
-    if rank == 0:
+    if w.rank == 0:
+        enc_shard, rec_shard = strides
         out = {
             "metric": "Encode + 1-lost Reconstruct GiB/s (device-resident), 12+4 @ 4KiB/1MiB",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": w.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
@@ -284,23 +504,42 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform random bytes generated on device, seeded per rank)",
             "config": {
-                "workload": (f"12+4 Encode + ReconstOne (k = step mod 12) of {n_enc} stripes "
-                             f"@ 4 KiB and of {n_rec} stripes @ 1 MiB, per GPU per step"),
+                "workload": (f"12+4 Encode + ReconstOne (k = step mod 12) of {args.enc_stripes} "
+                             f"stripes @ 4 KiB and of {args.rec_stripes} stripes @ 1 MiB, per GPU "
+                             f"per step"),
                 "data_shards": D, "parity_shards": P,
-                "encode_vect_bytes": ENC_S, "encode_stripes_per_gpu": n_enc,
-                "reconst_vect_bytes": REC_S, "reconst_stripes_per_gpu": n_rec,
+                "encode_vect_bytes": ENC_S, "encode_stripes_per_gpu": args.enc_stripes,
+                "reconst_vect_bytes": REC_S, "reconst_stripes_per_gpu": args.rec_stripes,
                 "encode_shard_stride": enc_shard, "reconst_shard_stride": rec_shard,
-                "parallelism": f"stripe split x{world}, no collective",
+                "parallelism": f"stripe split x{w.world}, no collective",
             },
             "rank_seconds": [round(v, 6) for v in rank_seconds],
             "kernels": kernels,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "config5": c5,
+            "host_e2e": he,
+            "xgmi_repair": xg,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    xdist.finalize()
+    return 0
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    try:
+        w = xdist.resolve_world(args.gpus)
+    except xdist.WorldMismatch as e:
+        log(f"bench.py: {e}")
+        return 2
+    if w.world > 1 and not w.launched:
+        # `python bench.py --gpus N` without torchrun: start the N ranks here,
+        # before this process makes any GPU call, and exit with their status.
+        argv = sys.argv[1:] if argv is None else list(argv)
+        return xdist.launch_local(w.world, [sys.executable, os.path.abspath(__file__)] + argv)
+    return run_rank(args, w)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

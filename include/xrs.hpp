@@ -57,6 +57,17 @@ inline std::vector<Slice> slices(Vects& v, size_t from = 0, size_t to = SIZE_MAX
   return out;
 }
 
+// Every non-null slice of `v` is `n` bytes long.  The C ABI reads and writes
+// `size` bytes of every vect, so a shorter one must be rejected here, before
+// the call (the Go dependency rejects mismatched vects too: ILLEGAL_VECTS).
+inline bool same_len(const std::vector<Slice>& v, size_t n) {
+  for (const Slice& s : v)
+    if (s.p && s.n != n) return false;
+  return true;
+}
+// Size check first (xrs.go:105 checkSize runs before the dependency's checks).
+inline bool lens_bad(const std::vector<Slice>& v, size_t n) { return !(n & 1) && !same_len(v, n); }
+
 class XRS {
  public:
   // xrs.go:55 New(dataNum, parityNum)
@@ -80,6 +91,7 @@ class XRS {
   Error Encode(std::vector<Slice> vects) {
     auto p = ptrs(vects);
     const size_t size = vects.empty() ? 0 : vects[0].n;
+    if (lens_bad(vects, size)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     return make_error(xrs_encode(c_, p.data(), static_cast<int>(p.size()), size),
                       static_cast<long long>(size));
   }
@@ -100,6 +112,7 @@ class XRS {
   Error ReconstOne(std::vector<Slice> vects, int k) {
     auto p = ptrs(vects);
     const size_t size = vects.empty() ? 0 : vects[0].n;
+    if (lens_bad(vects, size)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_reconst_one(c_, p.data(), static_cast<int>(p.size()), size, k);
     return make_error(rc, rc == XRS_ERR_SIZE_NOT_EVEN ? static_cast<long long>(size) : k);
   }
@@ -110,6 +123,7 @@ class XRS {
                 const std::vector<int>& need) {
     auto p = ptrs(vects);
     const size_t size = vects.empty() ? 0 : vects[0].n;
+    if (lens_bad(vects, size)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_reconst(c_, p.data(), static_cast<int>(p.size()), size, dp_has.data(),
                                static_cast<int>(dp_has.size()), need.data(),
                                static_cast<int>(need.size()));
@@ -123,6 +137,9 @@ class XRS {
   // xrs.go:324
   Error Update(const Vect& old_data, const Vect& new_data, int row, std::vector<Slice> parity) {
     auto p = ptrs(parity);
+    if (!(old_data.size() & 1) &&
+        (new_data.size() != old_data.size() || !same_len(parity, old_data.size())))
+      return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_update(c_, old_data.data(), new_data.data(), old_data.size(), row, p.data(),
                               static_cast<int>(p.size()));
     return make_error(rc, rc == XRS_ERR_SIZE_NOT_EVEN ? static_cast<long long>(old_data.size())
@@ -134,6 +151,7 @@ class XRS {
     auto d = ptrs(data);
     auto p = ptrs(parity);
     const size_t size = data.empty() ? 0 : data[0].n;
+    if (lens_bad(data, size) || lens_bad(parity, size)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_replace(c_, d.data(), rows.data(), static_cast<int>(rows.size()), size,
                                p.data(), static_cast<int>(p.size()));
     long long arg = 0;
@@ -179,6 +197,7 @@ class Queue {
   // xrs.go:103
   Error Encode(std::vector<Slice> vects) {
     auto p = ptrs(vects);
+    if (!same_len(vects, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     return make_error(xrs_queue_encode(q_, p.data(), static_cast<int>(p.size())),
                       static_cast<long long>(size_));
   }
@@ -186,6 +205,7 @@ class Queue {
   // xrs.go:175
   Error ReconstOne(std::vector<Slice> vects, int k) {
     auto p = ptrs(vects);
+    if (!same_len(vects, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     return make_error(xrs_queue_reconst_one(q_, p.data(), static_cast<int>(p.size()), k), k);
   }
   Error ReconstOne(Vects& vects, int k) { return ReconstOne(slices(vects), k); }
@@ -193,6 +213,7 @@ class Queue {
   Error Reconst(std::vector<Slice> vects, const std::vector<int>& dp_has,
                 const std::vector<int>& need) {
     auto p = ptrs(vects);
+    if (!same_len(vects, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_queue_reconst(q_, p.data(), static_cast<int>(p.size()), dp_has.data(),
                                      static_cast<int>(dp_has.size()), need.data(),
                                      static_cast<int>(need.size()));
@@ -206,6 +227,7 @@ class Queue {
   Error Replace(std::vector<Slice> data, const std::vector<int>& rows, std::vector<Slice> parity) {
     auto d = ptrs(data);
     auto p = ptrs(parity);
+    if (!same_len(data, size_) || !same_len(parity, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
     const int rc = xrs_queue_replace(q_, d.data(), rows.data(), static_cast<int>(rows.size()),
                                      p.data(), static_cast<int>(p.size()));
     long long arg = 0;
@@ -219,6 +241,8 @@ class Queue {
   // xrs.go:324
   Error Update(const Vect& old_data, const Vect& new_data, int row, std::vector<Slice> parity) {
     auto p = ptrs(parity);
+    if (old_data.size() != size_ || new_data.size() != size_ || !same_len(parity, size_))
+      return make_error(XRS_ERR_ILLEGAL_VECTS);
     return make_error(xrs_queue_update(q_, old_data.data(), new_data.data(), row, p.data(),
                                        static_cast<int>(p.size())),
                       row);

@@ -300,6 +300,32 @@ static void TestQueue_Concurrent() {
     FATAL("Update(row=d): got \"%s\"", e.msg.c_str());
 }
 
+// A vect shorter or longer than vects[0] is rejected before the C ABI call
+// (which reads and writes `size` bytes of every vect): ADVICE r1.
+static void TestMismatchedVects() {
+  std::unique_ptr<XRS> x;
+  if (Error e = XRS::New(kData, kParity, &x)) FATAL("New: %s", e.msg.c_str());
+  Vects v = new_shard_matrix(kData + kParity, 64);
+  v[14].resize(32);
+  if (Error e = x->Encode(v); !e || e.msg != "illegal vects") FATAL("Encode: \"%s\"", e.msg.c_str());
+  if (Error e = x->ReconstOne(v, 0); !e || e.msg != "illegal vects")
+    FATAL("ReconstOne: \"%s\"", e.msg.c_str());
+  if (Error e = x->Reconst(v, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11}, {12, 13}); !e || e.msg != "illegal vects")
+    FATAL("Reconst: \"%s\"", e.msg.c_str());
+  Vects par = new_shard_matrix(kParity, 64);
+  if (Error e = x->Update(Vect(64), Vect(63 + 1 - 2), 0, xrs::slices(par)); !e || e.msg != "illegal vects")
+    FATAL("Update: \"%s\"", e.msg.c_str());
+  Vects data = new_shard_matrix(2, 64);
+  data[1].resize(128);
+  if (Error e = x->Replace(xrs::slices(data), {0, 1}, xrs::slices(par)); !e || e.msg != "illegal vects")
+    FATAL("Replace: \"%s\"", e.msg.c_str());
+  // the even-size rule comes first (xrs.go:105)
+  Vects odd = new_shard_matrix(kData + kParity, 63);
+  odd[3].resize(10);
+  if (Error e = x->Encode(odd); !e || e.msg != "vect size not even: 63")
+    FATAL("Encode odd: \"%s\"", e.msg.c_str());
+}
+
 int main(int argc, char** argv) {
   const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
   struct T {
@@ -310,6 +336,7 @@ int main(int argc, char** argv) {
       {"TestMakeXORSet", TestMakeXORSet, false},
       {"TestXRS_GetNeedVects", TestXRS_GetNeedVects, false},
       {"TestErrors", TestErrors, false},
+      {"TestMismatchedVects", TestMismatchedVects, false},
       {"TestXRS_Encode", TestXRS_Encode, true},
       {"TestXRS_ReconstOne", TestXRS_ReconstOne, true},
       {"TestXRS_Reconst", TestXRS_Reconst, true},

@@ -103,6 +103,28 @@ def test_error_messages_are_go_text():
         x.encode([np.zeros(8, np.uint8) for _ in range(15)])
 
 
+def test_mismatched_vect_lengths_rejected_before_the_call():
+    """Every vect must be as long as vects[0] (the C ABI reads / writes that
+    many bytes of each): ADVICE r1.  The even-size rule is checked first."""
+    x = xrs_amd.XRS(12, 4)
+    v = [np.zeros(64, np.uint8) for _ in range(16)]
+    v[13] = np.zeros(32, np.uint8)
+    for call in (lambda: x.encode(v), lambda: x.reconst_one(v, 0),
+                 lambda: x.reconst(v, list(range(12)), [12, 13]),
+                 lambda: x.update(np.zeros(64, np.uint8), np.zeros(62, np.uint8), 0,
+                                  [np.zeros(64, np.uint8)] * 4),
+                 lambda: x.update(np.zeros(64, np.uint8), np.zeros(64, np.uint8), 0,
+                                  [np.zeros(64, np.uint8)] * 3 + [bytearray(65)]),
+                 lambda: x.replace([np.zeros(64, np.uint8), np.zeros(128, np.uint8)], [0, 1],
+                                   [np.zeros(64, np.uint8)] * 4)):
+        with pytest.raises(xrs_amd.XRSError, match="^illegal vects$"):
+            call()
+    odd = [np.zeros(63, np.uint8) for _ in range(16)]
+    odd[2] = np.zeros(10, np.uint8)
+    with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 63$"):
+        x.encode(odd)
+
+
 @pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
 def test_compute_without_gpu_fails_loudly():
     x = xrs_amd.XRS(12, 4)

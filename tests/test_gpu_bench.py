@@ -13,7 +13,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SMALL = ["--steps", "3", "--warmup", "1", "--enc-stripes", "2048", "--rec-stripes", "16",
-         "--no-cpu-baseline"]
+         "--no-cpu-baseline", "--config5-stripes", "64", "--config5-steps", "2", "--host-mib", "32",
+         "--xgmi-stripes", "4"]
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
         "cpu_baseline"}
@@ -40,6 +41,11 @@ def test_bench_one_gpu_contract():
     assert j["n_gpus"] == 1 and j["steps"] == 3 and j["value"] > 0
     assert j["roofline"]["bound"] == "hbm" and 0 < j["roofline"]["frac"] < 1
     assert set(j["kernels"]) == {"encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m"}
+    c5 = j["config5"]
+    assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok_rank0"]
+    assert len(c5["encode"]["rank_seconds"]) == 1 and c5["gibps"] > 0
+    assert set(j["host_e2e"]) >= {"encode_4k", "reconst_one_1m"}
+    assert "skipped" in j["xgmi_repair"]
 
 
 def test_bench_two_ranks_contract():
@@ -55,3 +61,22 @@ def test_bench_two_ranks_contract():
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert len(j["rank_seconds"]) == 2 and min(j["rank_seconds"]) > 0
     assert abs(j["ms_per_step"] * j["steps"] / 1e3 - max(j["rank_seconds"])) < 1e-3
+    assert j["config5"]["stripes_total"] == 128 and j["config5"]["roundtrip_ok_rank0"]
+    assert len(j["config5"]["reconst_one"]["rank_seconds"]) == 2
+    assert len(j["host_e2e"]["encode_4k"]["rank_gibps"]) == 2
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` without torchrun starts its two ranks itself (the
+    form the driver may use); on a one-GPU box they share cuda:0 over gloo."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["XRS_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _line(r.stdout)
+    assert j["n_gpus"] == 2 and len(j["rank_seconds"]) == 2 and min(j["rank_seconds"]) > 0
+    assert j["config5"]["stripes_total"] == 128
+    xg = j["xgmi_repair"]
+    assert ("skipped" in xg) or xg["xgmi_bitexact"]

@@ -46,6 +46,37 @@ def test_reconst_edge_vs_oracle(rng, has, need, size):
         assert np.array_equal(a[i], b[i]), i
 
 
+# Step-by-step plans that span more than one launch while a need row is also a
+# GF source (dp_has[:d]): no launch may read a row an earlier launch of the
+# plan wrote (codec.cpp step 3).
+MULTI_LAUNCH = [
+    (12, 4, list(range(0, 11)) + [13, 14, 15], [13, 0, 1, 2, 11]),  # > 4 needs, piggybacked survivor
+    (12, 4, list(range(0, 11)) + [13, 14, 15], [0, 13, 1, 11, 2, 12, 14]),
+    (12, 4, [i for i in range(16) if i not in (3, 7)], [3, 14, 13, 7, 5, 15]),
+    (30, 4, list(range(30)), [29, 31]),                              # d > kMaxSrc, need holds a survivor
+    (30, 4, [i for i in range(34) if i != 5], [5, 29, 32, 31, 0]),
+    (28, 6, [i for i in range(34) if i not in (1, 2)], [1, 30, 2, 0, 31, 33]),
+]
+
+
+@pytest.mark.parametrize("d,p,has,need", MULTI_LAUNCH)
+@pytest.mark.parametrize("size", [2, 4096, 1030])
+def test_reconst_multi_launch_aliasing_vs_oracle(rng, d, p, has, need, size):
+    o = OracleXRS(d, p)
+    v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d)]
+    v += [np.zeros(size, np.uint8) for _ in range(p)]
+    o.encode(v)
+    for i in range(d + p):
+        if i not in has:
+            v[i][:] = 0x5A
+    a = [r.copy() for r in v]
+    b = [r.copy() for r in v]
+    xrs_amd.XRS(d, p).reconst(a, has, need)
+    o.reconst(b, has, need)
+    for i in range(d + p):
+        assert np.array_equal(a[i], b[i]), i
+
+
 @pytest.mark.parametrize("has,need,msg", [
     (list(range(11)), [12, 13], "too few survivors"),
     (list(range(12)) + [16], [13, 14], "illegal index"),

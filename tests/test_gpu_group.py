@@ -89,3 +89,25 @@ def test_group_errors():
         g.reconst_one_host(buf.ctypes.data, 64, 64, 16 * 64, 1, 12)
     with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 63$"):
         g.encode_host(buf.ctypes.data, 63, 64, 16 * 64, 1)
+
+
+def test_group_replace_error_order_matches_codec():
+    """Too many rows and an odd size: the group and the single codec both
+    report the size first (check_replace order, as the oracle)."""
+    g = xrs_amd.XRSGroup(D, P, [0, 0])
+    x = xrs_amd.XRS(D, P)
+    data = np.zeros(64, np.uint8)
+    par = np.zeros(16 * 64, np.uint8)
+    rows = list(range(D + 1))
+    for call in (lambda: g.replace_host(data.ctypes.data, 0, 0, rows, 63, par.ctypes.data, 64,
+                                        4 * 64, 1),
+                 lambda: x.replace_host(data.ctypes.data, 0, 0, rows, 63, par.ctypes.data, 64,
+                                        4 * 64, 1)):
+        with pytest.raises(xrs_amd.XRSError, match="^vect size not even: 63$"):
+            call()
+    for call in (lambda: g.replace_host(data.ctypes.data, 0, 0, rows, 64, par.ctypes.data, 64,
+                                        4 * 64, 1),
+                 lambda: x.replace_host(data.ctypes.data, 0, 0, rows, 64, par.ctypes.data, 64,
+                                        4 * 64, 1)):
+        with pytest.raises(xrs_amd.XRSError, match="^illegal vects$"):
+            call()

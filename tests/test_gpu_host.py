@@ -184,3 +184,33 @@ def test_update_replace_host_vs_oracle(rng, monkeypatch, size, n, mode):
         x.update_host(sp, stripe, np_, size, size, 12, sp + D * size, size, stripe, n)
     for p_ in allocs:
         xrs_amd.lib().xrs_host_free(p_)
+
+
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pageable"])
+def test_reconst_host_negative_single_need_writes_nothing(rng, mode):
+    """need = [-1]: xrs.go:238 takes ReconstOne, which rejects k before any
+    write ('illegal data index: -1'); the host batch is left unchanged
+    (the general path used to run steps 1-2 in place first)."""
+    size, n = 4096, 64
+    stripe = 16 * size
+    if mode == "pageable":
+        buf = np.empty(n * stripe, np.uint8)
+        ptr = buf.ctypes.data
+    else:
+        ptr, buf = pinned(n * stripe)
+    buf[:] = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+    v = buf.reshape(n, 16, size)
+    OracleXRS(D, P).encode_batch(v, size, n)
+    v[:, 3] = 0x5A
+    before = buf.copy()
+    has = [j for j in range(D + P) if j != 3]
+    x = xrs_amd.XRS(D, P)
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: -1$"):
+        x.reconst_host(ptr, size, size, stripe, n, has, [-1])
+    assert np.array_equal(buf, before)
+    g = xrs_amd.XRSGroup(D, P, [0, 0])
+    with pytest.raises(xrs_amd.XRSError, match="^illegal data index: -1$"):
+        g.reconst_host(ptr, size, size, stripe, n, has, [-1])
+    assert np.array_equal(buf, before)
+    if mode != "pageable":
+        xrs_amd.lib().xrs_host_free(ptr)

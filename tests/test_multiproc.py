@@ -1,14 +1,19 @@
-"""World-size-2 gloo tests (CPU) of the multi-GPU path: the stripe split and
-the barrier/max-time bracket bench.py uses.  The per-rank compute is the CPU
-oracle here (the GPU box runs the kernels; 8-GPU runs are the driver's)."""
+"""Multi-rank tests (CPU, gloo, world size 2-3) of the harness bench.py runs
+on N GPUs (xrs_amd/dist.py): the rank layout and its --gpus check, the
+self-launch of `bench.py --gpus N`, the stripe split and the barrier +
+per-rank time bracket.  The per-rank compute is the CPU oracle here (the GPU
+box runs the kernels; 8-GPU runs are the driver's)."""
+import json
 import os
-import socket
+import subprocess
+import sys
 
-import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
-from xrs_amd.dist import stripe_range
+from xrs_amd import dist as xdist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "_rank_worker.py")
 
 
 def test_stripe_range_partitions():
@@ -16,57 +21,67 @@ def test_stripe_range_partitions():
         for world in (1, 2, 3, 8):
             seen = []
             for r in range(world):
-                s, c = stripe_range(n, r, world)
+                s, c = xdist.stripe_range(n, r, world)
                 seen.extend(range(s, s + c))
             assert seen == list(range(n))
     with pytest.raises(ValueError):
-        stripe_range(8, 2, 2)
+        xdist.stripe_range(8, 2, 2)
+    # config 5: 65,536 stripes over 8 GPUs = 8,192 each
+    assert [xdist.stripe_range(65536, r, 8)[1] for r in range(8)] == [8192] * 8
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def test_resolve_world():
+    w = xdist.resolve_world(None, env={})
+    assert (w.rank, w.world, w.launched) == (0, 1, False)
+    w = xdist.resolve_world(8, env={})
+    assert (w.rank, w.world, w.launched) == (0, 8, False)  # bench.py launches the 8 ranks
+    env = {"WORLD_SIZE": "4", "RANK": "3", "LOCAL_RANK": "3"}
+    w = xdist.resolve_world(4, env=env)
+    assert (w.rank, w.world, w.local, w.launched) == (3, 4, 3, True)
+    assert xdist.resolve_world(None, env=env).world == 4
+    with pytest.raises(xdist.WorldMismatch):
+        xdist.resolve_world(2, env=env)
+    with pytest.raises(xdist.WorldMismatch):
+        xdist.resolve_world(0, env={})
 
 
-def _worker(rank, world, port, n_stripes, size, out_dir):
-    import torch
-    import torch.distributed as dist
-
-    from oracle.oracle_c import OracleXRS
-    from xrs_amd.dist import stripe_range, timed_steps
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    rng = np.random.Generator(np.random.PCG64(42))
-    full = rng.integers(0, 256, size=(n_stripes, 16, size), dtype=np.uint8)
-    start, count = stripe_range(n_stripes, rank, world)
-    mine = full[start:start + count].copy()
-    o = OracleXRS(12, 4)
-
-    def step(i):
-        o.encode_batch(mine, size, count)
-
-    own, mx = timed_steps(step, steps=3, warmup=1, sync=lambda: None, device="cpu")
-    assert mx >= own
-    t = torch.from_numpy(mine.reshape(-1).copy())
-    sizes = [stripe_range(n_stripes, r, world)[1] * 16 * size for r in range(world)]
-    gathered = [torch.empty(s_, dtype=torch.uint8) for s_ in sizes]
-    # only the test gathers results; the benchmark path has no data collective
-    dist.all_gather(gathered, t) if len(set(sizes)) == 1 else [
-        dist.broadcast(gathered[r].copy_(t) if r == rank else gathered[r], src=r)
-        for r in range(world)]
-    if rank == 0:
-        got = np.concatenate([g.numpy() for g in gathered]).reshape(n_stripes, 16, size)
-        ref = full.copy()
-        o.encode_batch(ref, size, n_stripes)
-        np.save(os.path.join(out_dir, "ok.npy"), np.array([np.array_equal(got, ref), mx]))
-    dist.barrier()
-    dist.destroy_process_group()
+def test_bench_gpus_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 2
+    assert "--gpus 2" in r.stderr and "WORLD_SIZE=4" in r.stderr
+    assert not r.stdout.strip()
 
 
-@pytest.mark.parametrize("n_stripes", [64, 65])
-def test_two_rank_split_encode_gloo(tmp_path, n_stripes):
-    mp.spawn(_worker, args=(2, _free_port(), n_stripes, 4096, str(tmp_path)), nprocs=2, join=True)
-    ok, mx = np.load(tmp_path / "ok.npy")
-    assert ok == 1 and mx > 0
+def test_bench_self_launch_starts_n_ranks_without_gpu():
+    """`bench.py --gpus 2` without a launcher starts two rank processes; on
+    this GPU-less host each rank fails loudly (no CPU fallback) and the parent
+    returns a non-zero status."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1"], capture_output=True, text=True, timeout=180, env=env,
+                       cwd=ROOT)
+    assert r.returncode != 0
+    assert "needs a GPU" in r.stderr
+    assert not r.stdout.strip()
+
+
+@pytest.mark.parametrize("world,n_stripes", [(2, 64), (2, 65), (3, 65)])
+def test_launch_local_split_encode_gloo(tmp_path, world, n_stripes):
+    rc = xdist.launch_local(world, [sys.executable, WORKER, str(tmp_path), str(n_stripes), "4096"],
+                            timeout=240)
+    assert rc == 0
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert res["ok"] and res["world"] == world
+    assert len(res["rank_seconds"]) == world and min(res["rank_seconds"]) > 0
+    assert len(res["region_seconds"]) == world
+    assert sum(res["counts"]) == n_stripes
+
+
+def test_launch_local_propagates_a_failed_rank(tmp_path):
+    rc = xdist.launch_local(2, [sys.executable, WORKER, str(tmp_path), "8", "64", "1"],
+                            timeout=240)
+    assert rc == 3
+    assert not (tmp_path / "result.json").exists()

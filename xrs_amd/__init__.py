@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("XRS_LIB") or os.path.join(_HERE, "libxrs_hip.so")
 
 XRS_ERR_SIZE_NOT_EVEN = -2
 XRS_ERR_ILLEGAL_DATA_INDEX = -3
+XRS_ERR_ILLEGAL_VECTS = -4
 XRS_ERR_INVALID_ARG = -9
 
 
@@ -145,10 +146,31 @@ def _ptr(buf) -> int:
     return ctypes.addressof(buf)
 
 
+def _nbytes(buf) -> int:
+    if hasattr(buf, "nbytes"):
+        return int(buf.nbytes)
+    if isinstance(buf, (bytearray, bytes)):
+        return len(buf)
+    return ctypes.sizeof(buf)
+
+
+def _check_lens(size: int, *groups, exact: bool = False) -> None:
+    """Every (non-None) vect in `groups` is `size` bytes: the C ABI reads and
+    writes `size` bytes of each, so a shorter one would be overrun.  Checked
+    after the even-size rule (xrs.go:105 checkSize runs first) unless `exact`
+    (a queue's fixed size)."""
+    if size & 1 and not exact:
+        return
+    for g in groups:
+        for v in g:
+            if v is not None and _nbytes(v) != size:
+                raise XRSError(XRS_ERR_ILLEGAL_VECTS, "illegal vects")
+
+
 def _ptrs(vects):
     a = (ctypes.c_void_p * max(1, len(vects)))()
     for i, v in enumerate(vects):
-        a[i] = _ptr(v)
+        a[i] = None if v is None else _ptr(v)
     return a
 
 
@@ -226,29 +248,34 @@ class XRS:
 
     # ------------------------------------------------------- sync (host) API
     def encode(self, vects) -> None:
-        size = len(vects[0]) if len(vects) else 0
+        size = _nbytes(vects[0]) if len(vects) else 0
+        _check_lens(size, vects)
         _raise(_lib.xrs_encode(self._h, _ptrs(vects), len(vects), size), size)
 
     def reconst_one(self, vects, need_reconst: int) -> None:
-        size = len(vects[0])
+        size = _nbytes(vects[0])
+        _check_lens(size, vects)
         rc = _lib.xrs_reconst_one(self._h, _ptrs(vects), len(vects), size, int(need_reconst))
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else need_reconst)
 
     def reconst(self, vects, dp_has, need_reconst) -> None:
-        size = len(vects[0])
+        size = _nbytes(vects[0])
+        _check_lens(size, vects)
         rc = _lib.xrs_reconst(self._h, _ptrs(vects), len(vects), size, _ints(dp_has),
                               len(dp_has), _ints(need_reconst), len(need_reconst))
         arg = size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
         _raise(rc, arg)
 
     def update(self, old_data, new_data, row: int, parity) -> None:
-        size = len(old_data)
+        size = _nbytes(old_data)
+        _check_lens(size, [new_data], parity)
         rc = _lib.xrs_update(self._h, _ptr(old_data), _ptr(new_data), size, int(row),
                              _ptrs(parity), len(parity))
         _raise(rc, size if rc == XRS_ERR_SIZE_NOT_EVEN else row)
 
     def replace(self, data, replace_rows, parity) -> None:
-        size = len(data[0]) if len(data) else 0
+        size = _nbytes(data[0]) if len(data) else 0
+        _check_lens(size, data, parity)
         rc = _lib.xrs_replace(self._h, _ptrs(data), _ints(replace_rows), len(replace_rows), size,
                               _ptrs(parity), len(parity))
         bad = next((r for r in replace_rows if r < 0 or r >= self.data_num), 0)
@@ -469,25 +496,30 @@ class XRSQueue:
                 self._cv.notify_all()
 
     def encode(self, vects) -> None:
+        _check_lens(self.size, vects, exact=True)
         _raise(self._call(_lib.xrs_queue_encode, _ptrs(vects), len(vects)), self.size)
 
     def reconst_one(self, vects, need_reconst: int) -> None:
+        _check_lens(self.size, vects, exact=True)
         _raise(self._call(_lib.xrs_queue_reconst_one, _ptrs(vects), len(vects),
                           int(need_reconst)), need_reconst)
 
     def reconst(self, vects, dp_has, need_reconst) -> None:
+        _check_lens(self.size, vects, exact=True)
         rc = self._call(_lib.xrs_queue_reconst, _ptrs(vects), len(vects), _ints(dp_has),
                         len(dp_has), _ints(need_reconst), len(need_reconst))
         arg = self.size if rc == XRS_ERR_SIZE_NOT_EVEN else (need_reconst[0] if need_reconst else 0)
         _raise(rc, arg)
 
     def replace(self, data, replace_rows, parity) -> None:
+        _check_lens(self.size, data, parity, exact=True)
         rc = self._call(_lib.xrs_queue_replace, _ptrs(data), _ints(replace_rows),
                         len(replace_rows), _ptrs(parity), len(parity))
         bad = next((r for r in replace_rows if r < 0 or r >= self._codec.data_num), 0)
         _raise(rc, bad)
 
     def update(self, old_data, new_data, row: int, parity) -> None:
+        _check_lens(self.size, [old_data, new_data], parity, exact=True)
         _raise(self._call(_lib.xrs_queue_update, _ptr(old_data), _ptr(new_data), int(row),
                           _ptrs(parity), len(parity)), row)
 

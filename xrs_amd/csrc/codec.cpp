@@ -447,23 +447,47 @@ int reconst_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stri
       rep[it - uniq.begin()]++;
     }
   }
-  std::vector<RowRef> dst;
-  for (int t : uniq) dst.push_back(L.row(t, half));
+  // A need row that is one of the d GF sources (dp_has[:d]) rebuilds as
+  // itself: its coefficient row is a unit vector.  It is kept out of the GF
+  // plan, so no launch of a multi-launch plan (more than kMaxOut outputs, or
+  // d > kMaxSrc chained launches) reads a source row an earlier launch of the
+  // same plan already wrote; its re-piggyback XOR (if any) is applied after
+  // every GF output is written.  The oracle computes all outputs before
+  // writing any (oracle/xrs_oracle.c oxrs_rs_reconst), which this matches.
+  std::vector<RowRef> dst, self_dst;
+  std::vector<int> gf_u, self_u;
+  for (size_t u = 0; u < uniq.size(); ++u) {
+    const bool is_src = std::find(dp_has, dp_has + d, uniq[u]) != dp_has + d;
+    (is_src ? self_u : gf_u).push_back(static_cast<int>(u));
+  }
   std::vector<MulSrc> ms(d);
   for (int m = 0; m < d; ++m) {
     ms[m].row = L.row(dp_has[m], half);
-    ms[m].coef.resize(uniq.size());
-    for (size_t u = 0; u < uniq.size(); ++u) ms[m].coef[u] = coef[qidx[u]][m];
     ms[m].pb = -1;
+    for (int u : gf_u) ms[m].coef.push_back(coef[qidx[u]][m]);
   }
-  std::vector<XorSrc> xs;
-  for (size_t u = 0; u < uniq.size(); ++u) {
-    const int t = uniq[u];
+  std::vector<XorSrc> xs, self_xs;
+  for (int u : gf_u) {
+    const int o = static_cast<int>(dst.size()), t = uniq[u];
+    dst.push_back(L.row(t, half));
     if (t <= d || (rep[u] & 1) == 0) continue;
-    for (int ai : x->xs[t]) xs.push_back({L.row(ai, 0), {static_cast<int>(u)}});
+    for (int ai : x->xs[t]) xs.push_back({L.row(ai, 0), {o}});
   }
-  e = run_rows(dst, ms, xs, false, half, n_stripes, s);
-  if (e) return e;
+  for (int u : self_u) {
+    const int t = uniq[u];
+    if (t <= d || (rep[u] & 1) == 0 || x->xs[t].empty()) continue;  // unchanged
+    const int o = static_cast<int>(self_dst.size());
+    self_dst.push_back(L.row(t, half));
+    for (int ai : x->xs[t]) self_xs.push_back({L.row(ai, 0), {o}});
+  }
+  if (!dst.empty()) {
+    e = run_rows(dst, ms, xs, false, half, n_stripes, s);
+    if (e) return e;
+  }
+  if (!self_dst.empty()) {
+    e = run_rows(self_dst, {}, self_xs, true, half, n_stripes, s);
+    if (e) return e;
+  }
   for (int t : uniq) w->add(t, 1);
   return XRS_OK;
 }
@@ -1258,7 +1282,7 @@ int xrs_reconst_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t
                      const int* need, int n_need) {
   if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
     return XRS_ERR_INVALID_ARG;
-  if (n_need == 1 && need[0] >= 0 && need[0] < x->d)  // xrs.go:238-240
+  if (n_need == 1 && need[0] < x->d)  // xrs.go:238-240 (a negative k is rejected there)
     return xrs_reconst_one_host(x, host_base, size, shard_stride, stripe_stride, n_stripes,
                                 need[0]);
   int e = check_size(size);

@@ -144,7 +144,11 @@ int xrs_group_reconst_one_host(xrs_group* g, uint8_t* host_base, size_t size, si
 int xrs_group_reconst_host(xrs_group* g, uint8_t* host_base, size_t size, size_t shard_stride,
                            size_t stripe_stride, size_t n_stripes, const int* dp_has, int n_has,
                            const int* need, int n_need) {
-  if (!g) return XRS_ERR_INVALID_ARG;
+  if (!g || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] < xrs_data_num(g->codecs[0]))  // xrs.go:238-240
+    return xrs_group_reconst_one_host(g, host_base, size, shard_stride, stripe_stride, n_stripes,
+                                      need[0]);
   if (size & 1) return XRS_ERR_SIZE_NOT_EVEN;
   if (n_stripes == 0 || size == 0) return XRS_OK;
   if (!host_base) return XRS_ERR_INVALID_ARG;
@@ -178,8 +182,10 @@ int xrs_group_replace_host(xrs_group* g, const uint8_t* data_base, size_t data_s
                            uint8_t* parity_base, size_t parity_shard_stride,
                            size_t parity_stripe_stride, size_t n_stripes) {
   if (!g) return XRS_ERR_INVALID_ARG;
-  if (n < 1 || n > xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_VECTS;
+  // same order as the single codec's check_replace (codec.cpp) and the oracle
+  if (n < 1) return XRS_ERR_ILLEGAL_VECTS;
   if (size & 1) return XRS_ERR_SIZE_NOT_EVEN;
+  if (n > xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_VECTS;
   if (!rows) return XRS_ERR_INVALID_ARG;
   for (int i = 0; i < n; ++i)
     if (rows[i] < 0 || rows[i] >= xrs_data_num(g->codecs[0])) return XRS_ERR_ILLEGAL_DATA_INDEX;

@@ -445,7 +445,7 @@ int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_
   if (!q) return XRS_ERR_INVALID_ARG;
   if (n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
     return XRS_ERR_INVALID_ARG;
-  if (n_need == 1 && need[0] >= 0 && need[0] < q->d)  // xrs.go:238-240
+  if (n_need == 1 && need[0] < q->d)  // xrs.go:238-240 (a negative k is rejected there)
     return xrs_queue_reconst_one(q, vects, n, need[0]);
   const int d = q->d, m = q->d + q->p;
   if (!vects || n != m) return XRS_ERR_ILLEGAL_VECTS;

@@ -31,9 +31,9 @@ After the headline timed region, the same line carries:
     per-rank times;
   * "host_e2e": the host-resident path (shards start and end in pinned host
     memory, xrs_*_host, PCIe-inclusive) on every rank at once;
-  * "xgmi_repair" (N >= 2, two visible GPUs): rank 0 rebuilds a data shard
-    with half of its need set on the peer GPU (xGMI reads), checked bit for
-    bit against the same rebuild from local shards.
+  * "xgmi_repair" (two or more visible GPUs): rank 0 (in a child process)
+    rebuilds a data shard with half of its need set on the peer GPU (xGMI
+    reads), checked bit for bit against the rebuild from local shards.
 
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
 """
@@ -172,6 +172,7 @@ def parse_args(argv=None):
                     help="MiB per host-resident batch for the host_e2e key (0: skip)")
     ap.add_argument("--xgmi-stripes", type=int, default=64,
                     help="1 MiB stripes for the xgmi_repair key (0: skip)")
+    ap.add_argument("--xgmi-child", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--ramp-seconds", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -396,12 +397,13 @@ def xgmi_repair(R: Rank, args):
     the result bit for bit against the rebuild from all-local shards.
     Semantics: xrs.go:175-221."""
     torch, x, s = R.torch, R.x, R.stream
-    if R.ndev < 2:
-        return {"skipped": f"{R.ndev} GPU visible to rank 0"}
+    # XRS_XGMI_SELF=1 on a one-GPU box: the "peer" is the same device (every
+    # step but the xGMI reads themselves; tests/test_gpu_bench.py)
     peer = (R.dev_index + 1) % R.ndev
-    rc = R.xrs_amd.lib().xrs_enable_peer_access(R.dev_index, peer)
-    if rc != 0:
-        return {"skipped": f"peer access {R.dev_index}->{peer} unavailable (code {rc})"}
+    if peer != R.dev_index:
+        rc = R.xrs_amd.lib().xrs_enable_peer_access(R.dev_index, peer)
+        if rc != 0:
+            return {"skipped": f"peer access {R.dev_index}->{peer} unavailable (code {rc})"}
     n, size, k = args.xgmi_stripes, REC_S, 4
     col = n * size  # shard-major: shard i of stripe t at base + i*col + t*size
     local = R.random_bytes((D + P) * col, 0x961)
@@ -448,6 +450,34 @@ def xgmi_repair(R: Rank, args):
             "bytes_per_call": n * 9 * size}
 
 
+def run_xgmi_child(args, device: int, ndev: int):
+    """xgmi_repair in a child process (rank 0 only, other ranks wait at a
+    barrier), so that a fault on the peer path cannot take the bench line
+    with it; the child's JSON line (or its failure) becomes the key."""
+    import subprocess
+
+    if ndev < 2 and not os.environ.get("XRS_XGMI_SELF"):
+        return {"skipped": f"{ndev} GPU visible to rank 0 (cross-GPU repair needs two)"}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--xgmi-child", str(device),
+           "--xgmi-stripes", str(args.xgmi_stripes)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 240 s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-800:]}
+    return json.loads(lines[-1])
+
+
+def xgmi_child(args) -> int:
+    R = Rank(xdist.World(0, 1, args.xgmi_child, False), "none")
+    print(json.dumps(xgmi_repair(R, args)), flush=True)
+    return 0
+
+
 def run_rank(args, w):
     backend = os.environ.get("XRS_DIST_BACKEND", "nccl")
     R = Rank(w, backend)
@@ -475,13 +505,11 @@ def run_rank(args, w):
         c5, _ = config5(R, args)
     he = host_e2e(R, args) if args.host_mib > 0 else None
     xg = None
-    if w.world > 1 and args.xgmi_stripes > 0:
+    if args.xgmi_stripes > 0:
         xdist.barrier()
         if w.rank == 0:
-            xg = xgmi_repair(R, args)
+            xg = run_xgmi_child(args, R.dev_index, R.ndev)
         xdist.barrier()
-    elif args.xgmi_stripes > 0:
-        xg = {"skipped": "N = 1 (cross-GPU repair runs at N >= 2)"}
 
     cpu = None
     if w.rank == 0 and w.world == 1 and not args.no_cpu_baseline:
@@ -528,6 +556,8 @@ def run_rank(args, w):
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.xgmi_child is not None:  # rank 0's isolated cross-GPU repair probe
+        return xgmi_child(args)
     try:
         w = xdist.resolve_world(args.gpus)
     except xdist.WorldMismatch as e:

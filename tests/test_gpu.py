@@ -493,3 +493,73 @@ def test_golden_codecs_gpu(golden_codecs, cuda, d, p, S):
     par = [r.copy() for r in g[k + "rp_in"]]
     x.replace([r.copy() for r in g[k + "rp_data"]], [int(j) for j in g[k + "rp_rows"]], par)
     assert np.array_equal(np.stack(par), g[k + "rp_out"])
+
+
+@pytest.mark.parametrize("tail", ["overlap", "launch"])
+@pytest.mark.parametrize("size,n", [(4100, 300), (1048578, 3), (34, 500), (18, 200), (4126, 100),
+                                    (4098, 100), (65538, 20)])
+def test_ragged_sizes_encode_reconst_one_vs_oracle(cuda, rng, monkeypatch, tail, size, n):
+    """Vect sizes whose half is not a multiple of 16 (xrs.go:130-136 accepts
+    any even size).  "overlap": the 16-byte launch ends with one overlapping
+    chunk per row (the default); "launch": the separate byte-granular tail
+    launch (XRS_TAIL=launch).  Both against the oracle, bytes between
+    shards untouched (padded layout, odd strides)."""
+    if tail == "launch":
+        monkeypatch.setenv("XRS_TAIL", "launch")
+    o = OracleXRS(D, P)
+    x = xrs_amd.XRS(D, P)
+    for shard_stride in (size, size + 7):
+        stripe_stride = 16 * shard_stride + 3
+        buf = rng.integers(0, 256, size=n * stripe_stride, dtype=np.uint8)
+        t = to_dev(buf, cuda)
+        x.encode_batched(t.data_ptr(), size, shard_stride, stripe_stride, n, stream())
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        ref = buf.copy()
+        for s in range(n):
+            v = [ref[s * stripe_stride + i * shard_stride:][:size].copy() for i in range(D + P)]
+            o.encode(v)
+            for i in range(D + P):
+                off = s * stripe_stride + i * shard_stride
+                ref[off:off + size] = v[i]
+        assert np.array_equal(got, ref)  # shards encoded, gaps untouched
+        for k in (0, 7, 11):
+            h = ref.copy()
+            for s in range(n):
+                off = s * stripe_stride + k * shard_stride
+                h[off:off + size] = 0x5A
+            t = to_dev(h, cuda)
+            x.reconst_one_batched(t.data_ptr(), size, shard_stride, stripe_stride, n, k, stream())
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), ref), (shard_stride, k)
+
+
+CT_CODECS = [(4, 2), (6, 3), (8, 4), (10, 4), (12, 3), (14, 4), (16, 4), (20, 4), (10, 2), (6, 2),
+             (8, 3), (10, 3), (12, 2)]
+
+
+@pytest.mark.parametrize("mode", ["ct", "dyn"])
+@pytest.mark.parametrize("d,p", CT_CODECS)
+def test_compile_time_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, p):
+    """The compile-time Encode (pair_kernel<p, d>) and ReconstOne
+    (rows_kernel<2, d, |XORSet(bi)|>) shapes of common codecs, and the
+    runtime-count kernels they replace (XRS_ENCODE_DYN / XRS_ROWS_DYN), on
+    batches against the oracle: every k, aligned and ragged sizes."""
+    if mode == "dyn":
+        monkeypatch.setenv("XRS_ENCODE_DYN", "1")
+        monkeypatch.setenv("XRS_ROWS_DYN", "1")
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    for size, n in ((4096, 64), (4100, 33), (34, 50)):
+        host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+        t = to_dev(host, cuda)
+        x.encode_batched(t.data_ptr(), size, size, (d + p) * size, n, stream())
+        ref = host.copy()
+        o.encode_batch(ref, size, n)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), ref), size
+        for k in range(d):
+            t = to_dev(ref, cuda)
+            t[:, k] = 0x5A
+            x.reconst_one_batched(t.data_ptr(), size, size, (d + p) * size, n, k, stream())
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), ref), (size, k)

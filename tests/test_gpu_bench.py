@@ -45,7 +45,22 @@ def test_bench_one_gpu_contract():
     assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok_rank0"]
     assert len(c5["encode"]["rank_seconds"]) == 1 and c5["gibps"] > 0
     assert set(j["host_e2e"]) >= {"encode_4k", "reconst_one_1m"}
-    assert "skipped" in j["xgmi_repair"]
+    xg = j["xgmi_repair"]
+    assert ("skipped" in xg) or xg["xgmi_bitexact"], xg
+
+
+def test_bench_xgmi_child_self_peer():
+    """The cross-GPU repair probe end to end on one card (XRS_XGMI_SELF: the
+    "peer" shards are a second allocation on the same device), so the path
+    the driver's multi-GPU run takes is exercised here."""
+    env = dict(os.environ, XRS_XGMI_SELF="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL
+                       + ["--config5-stripes", "0", "--host-mib", "0"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    xg = _line(r.stdout)["xgmi_repair"]
+    assert xg["xgmi_bitexact"] is True, xg
+    assert xg["gbs_algorithmic"] > 0 and xg["gbs_all_local"] > 0
 
 
 def test_bench_two_ranks_contract():

@@ -145,6 +145,39 @@ def main():
                 emit(f"reconst_one_{d}+{p}", size, n, secs,
                      n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
                 del t
+    if "others_ab" in cases:  # other (d, p): compile-time shapes vs runtime-count kernels
+        for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3), (14, 4), (10, 2)):
+            xo = xrs_amd.XRS(d, p)
+            for size in (4096, 1 << 20):
+                n = (4 << 30) // ((d + p) * size)
+                shard, stripe = xrs_amd.batch_strides(size, d + p)
+                t = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device=dev)
+                ks = sorted({0, d - 1})
+                best = {}
+                for rnd in range(2):  # interleaved A/B rounds, best of each
+                    for mode in ("ct", "dyn"):
+                        for var in ("XRS_ENCODE_DYN", "XRS_ROWS_DYN"):
+                            if mode == "dyn":
+                                os.environ[var] = "1"
+                            else:
+                                os.environ.pop(var, None)
+                        sec = timed(lambda i: xo.encode_batched(t.data_ptr(), size, shard, stripe,
+                                                                n, s))
+                        best[("enc", mode)] = min(best.get(("enc", mode), 1e9), sec)
+                        for k in ks:
+                            sec = timed(lambda i: xo.reconst_one_batched(t.data_ptr(), size, shard,
+                                                                         stripe, n, k, s))
+                            best[(k, mode)] = min(best.get((k, mode), 1e9), sec)
+                for var in ("XRS_ENCODE_DYN", "XRS_ROWS_DYN"):
+                    os.environ.pop(var, None)
+                for mode in ("ct", "dyn"):
+                    emit(f"encode_{d}+{p}_{mode}", size, n, best[("enc", mode)],
+                         n * (d + p) * size, shard)
+                    for k in ks:
+                        a_need, _ = xo.get_need_vects(k)
+                        emit(f"reconst_one_{d}+{p}_k{k}_{mode}", size, n, best[(k, mode)],
+                             n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
+                del t
     torch.cuda.empty_cache()
 
 

@@ -74,7 +74,7 @@ struct XorSrc {
 // Pair plans: outputs in groups of kMaxOut, sources in chunks of kMaxSrc; the
 // first chunk of each group writes (or accumulates if acc), later chunks add.
 int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, bool acc,
-             bool encode12, uint64_t half, uint64_t n_stripes, hipStream_t stream) {
+             bool encode, uint64_t half, uint64_t n_stripes, hipStream_t stream) {
   if (half == 0 || n_stripes == 0 || dst.empty()) return XRS_OK;
   const GF& gf = GF::get();
   const int np = static_cast<int>(dst.size()), ns = static_cast<int>(src.size());
@@ -88,7 +88,9 @@ int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, boo
       plan.P = P;
       plan.C = C;
       plan.acc = acc || c0 > 0;
-      plan.encode12 = encode12 && np == 4 && ns == 12;
+      // one launch covers the whole Encode: source c = data c, piggyback
+      // target 1 + c % (p-1) (makeXORSet, xrs.go:77-100)
+      plan.encode_xs = encode && np <= xrs::kMaxOut && ns <= xrs::kMaxSrc;
       plan.half = half;
       plan.n_stripes = n_stripes;
       for (int r = 0; r < P; ++r) plan.dst[r] = dst[g0 + r];
@@ -248,7 +250,7 @@ int encode_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_strip
     for (int r = 0; r < p; ++r) src[j].coef[r] = x->g(d + r, j);
     src[j].pb = x->bi_of[j] - d;  // xrs.go:118-126 piggyback target
   }
-  return run_pair(dst, src, false, d == 12 && p == 4, half, n_stripes, s);
+  return run_pair(dst, src, false, true, half, n_stripes, s);
 }
 
 int reconst_one_impl(const xrs_codec* x, const Layout& L, size_t size, size_t n_stripes, int k,

@@ -24,6 +24,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 
 #include "gf256.h"
 #include "xrs_plan.h"
@@ -148,6 +149,7 @@ struct PairArgs {
   uint64_t chunks;  // lanes per stripe
   uint64_t total;   // n_stripes * chunks
   uint64_t off0;    // first byte of each half this launch covers
+  uint64_t last;    // ragged end: the last chunk starts here (overlap), else ~0
 };
 
 template <int P, int W>
@@ -216,7 +218,8 @@ __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
   const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
   uint32_t acc_a[P][W], acc_b[P][W];
@@ -247,9 +250,10 @@ __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
     for (int c = 0; c + 1 < C; c += 2)
       pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
     if constexpr (C & 1) pair_mac1<P, W>(acc_a, acc_b, a.tab[C - 1], xa[C - 1], xb[C - 1]);
-    if constexpr (C == 12 && !ACC) {
+    if constexpr (!ACC) {
       // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
-      // c rides on parity 1 + c % (P-1).  Only used for full-width Encode.
+      // c rides on parity 1 + c % (P-1).  Compile-time source counts are only
+      // launched for a whole Encode (PairPlan::encode_xs).
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -307,6 +311,7 @@ struct RowsArgs {
   uint64_t chunks;
   uint64_t total;
   uint64_t off0;
+  uint64_t last;  // ragged end: the last chunk starts here (overlap), else ~0
 };
 
 template <int R, int W>
@@ -352,7 +357,8 @@ __global__ __launch_bounds__(BS) void rows_kernel(const RowsArgs<R, NM, NX, VEC>
   const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
   const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
 
   uint32_t acc[R][W];
@@ -853,7 +859,8 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   a.n_src = n;
   a.half = p.half;
   a.off0 = p.off0;
-  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
+  a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
+  a.last = (VEC && p.overlap) ? p.end - 16 : ~uint64_t(0);
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   // 128-thread blocks for the 16-byte kernels on halves up to 4 KiB (Encode
@@ -879,10 +886,38 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   return static_cast<int>(hipGetLastError());
 }
 
+// Compile-time source counts per output count for a whole Encode (every load
+// issued before the first multiply): 12+4 (the headline) and the common
+// codecs around it.  Anything else runs the runtime-count kernel.
+template <int P>
+struct EncodeShapes;
+template <>
+struct EncodeShapes<2> {
+  using type = std::integer_sequence<int, 4, 6, 8, 10, 12>;
+};
+template <>
+struct EncodeShapes<3> {
+  using type = std::integer_sequence<int, 6, 8, 10, 12>;
+};
+template <>
+struct EncodeShapes<4> {
+  using type = std::integer_sequence<int, 8, 10, 12, 14, 16, 20>;
+};
+
+template <int P, bool VEC, int... Cs>
+int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int, Cs...>) {
+  int rc = -1;
+  (void)((p.C == Cs && (rc = launch_pair_t<P, Cs, false, VEC>(p, s), true)) || ...);
+  return rc;
+}
+
 template <int P, bool ACC, bool VEC>
 int launch_pair_c(const PairPlan& p, hipStream_t s) {
-  if constexpr (P == 4 && !ACC) {
-    if (p.C == 12 && p.encode12) return launch_pair_t<4, 12, ACC, VEC>(p, s);  // 12+4 Encode
+  if constexpr (!ACC && VEC && P >= 2) {
+    if (p.encode_xs && !std::getenv("XRS_ENCODE_DYN")) {
+      const int rc = launch_encode_ct<P, VEC>(p, s, typename EncodeShapes<P>::type{});
+      if (rc != -1) return rc;
+    }
   }
   // (Compile-time Update (C=2) and Replace(4) shapes measured no faster than
   // the runtime kernel at 8 MiB: profiles/r01_bench_configs_c4_ct.log.)
@@ -916,7 +951,8 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   a.nx = p.NX;
   a.len = p.len;
   a.off0 = p.off0;
-  a.chunks = VEC ? (p.end - p.off0) / 16 : (p.end - p.off0 + 3) / 4;
+  a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
+  a.last = (VEC && p.overlap) ? p.end - 16 : ~uint64_t(0);
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   // 1024-thread blocks for rows of >= 256 KiB (ReconstOne at 1 MiB vects:
@@ -941,10 +977,35 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   return static_cast<int>(hipGetLastError());
 }
 
+// Compile-time (NM, NX) of ReconstOne (two outputs; NM = d survivors' b-halves,
+// NX = |XORSet(bi)| rows XORed in) for 12+4 (the headline) and the common
+// codecs: (d, p) -> NX in {floor, ceil}(d / (p-1)).
+template <int NM, int NX>
+struct Shape2 {};
+template <bool VEC, int... NMs, int... NXs>
+int launch_reconst_one_ct(const RowsPlan& p, hipStream_t s, Shape2<NMs, NXs>...) {
+  int rc = -1;
+  (void)(((p.NM == NMs && p.NX == NXs) && (rc = launch_rows_t<2, NMs, NXs, false, VEC>(p, s), true)) ||
+         ...);
+  return rc;
+}
+
 template <int R, bool ACC, bool VEC>
 int launch_rows_c(const RowsPlan& p, hipStream_t s) {
-  if constexpr (R == 2 && !ACC && VEC) {  // (the byte path of this shape would use scratch)
-    if (p.NM == 12 && p.NX == 4) return launch_rows_t<2, 12, 4, ACC, VEC>(p, s);  // 12+4 ReconstOne
+  if constexpr (R == 2 && !ACC && VEC) {  // (the byte path of these shapes would use scratch)
+    if (!std::getenv("XRS_ROWS_DYN")) {
+      const int rc = launch_reconst_one_ct<VEC>(
+          p, s, Shape2<12, 4>{},                     // 12+4
+          Shape2<4, 4>{}, Shape2<6, 3>{},            // 4+2, 6+3
+          Shape2<8, 2>{}, Shape2<8, 3>{},            // 8+4
+          Shape2<10, 3>{}, Shape2<10, 4>{},          // 10+4
+          Shape2<12, 6>{},                           // 12+3
+          Shape2<14, 4>{}, Shape2<14, 5>{},          // 14+4
+          Shape2<16, 5>{}, Shape2<16, 6>{},          // 16+4
+          Shape2<20, 6>{}, Shape2<20, 7>{},          // 20+4
+          Shape2<10, 10>{});                         // 10+2
+      if (rc != -1) return rc;
+    }
   }
   return launch_rows_t<R, kDyn, kDyn, ACC, VEC>(p, s);
 }
@@ -969,11 +1030,27 @@ int launch_rows_r(const RowsPlan& p, hipStream_t s) {
 // (4-5x slower: profiles/r01_odd_probe.log).  XRS_UNALIGNED_VEC=0 restores
 // the strict rule for A/B runs: 16-byte kernels only when every row, stride
 // and len is 16-byte aligned.
+//
+// Ragged end without a second launch (`overlap_ok`: the launch writes each
+// output byte as a pure function of input bytes at the same offset, i.e. no
+// accumulate and no output row that is also an input row): when len >= 16 is
+// not a multiple of 16, the 16-byte launch covers [0, len) with one more
+// chunk per row, starting at len - 16.  It overlaps the previous chunk, whose
+// bytes it rewrites with the same values.  The separate byte-granular tail
+// launch touched one line per row per stripe and cost 10-35% at 4,100-byte
+// vects (profiles/r01_odd_probe.log).  XRS_TAIL=launch restores it (A/B).
 template <class Plan, class F>
-int split_launch(Plan p, uint64_t len, bool aligned, F launch) {
+int split_launch(Plan p, uint64_t len, bool aligned, F launch, bool overlap_ok = false) {
   const char* e = std::getenv("XRS_UNALIGNED_VEC");
   uint64_t bulk = len & ~uint64_t(15);
   if (e && e[0] == '0' && !(aligned && bulk == len)) bulk = 0;
+  const char* tv = std::getenv("XRS_TAIL");
+  if (overlap_ok && bulk && bulk < len && !(tv && std::strcmp(tv, "launch") == 0)) {
+    p.off0 = 0;
+    p.end = len;
+    p.overlap = true;
+    return launch(p, true);
+  }
   int rc = 0;
   if (bulk) {
     p.off0 = 0;
@@ -990,6 +1067,14 @@ int split_launch(Plan p, uint64_t len, bool aligned, F launch) {
 
 bool row_aligned(const RowRef& r) { return aligned16(r.ptr) && aligned16(r.stripe_stride); }
 
+// Two rows of `len` bytes (stripe 0) share a byte, or step differently
+// (then assume they may meet in some stripe).
+bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len) {
+  if (a.stripe_stride != b.stripe_stride) return true;
+  const uint64_t lo = a.ptr < b.ptr ? a.ptr : b.ptr, hi = a.ptr < b.ptr ? b.ptr : a.ptr;
+  return hi - lo < len;
+}
+
 }  // namespace
 
 int launch_pair(const PairPlan& p0, void* stream) {
@@ -998,10 +1083,15 @@ int launch_pair(const PairPlan& p0, void* stream) {
   bool al = true;
   for (int c = 0; c < p0.C; ++c) al = al && row_aligned(p0.src[c]);
   for (int r = 0; r < p0.P; ++r) al = al && row_aligned(p0.dst[r]);
-  return split_launch(p0, p0.half, al, [s](const PairPlan& p, bool vec) {
+  PairPlan pp = p0;
+  pp.overlap = false;
+  bool pure = !p0.acc;  // no accumulate, and no destination that is also a source
+  for (int r = 0; r < p0.P && pure; ++r)
+    for (int c = 0; c < p0.C && pure; ++c) pure = !rows_overlap(p0.dst[r], p0.src[c], 2 * p0.half);
+  return split_launch(pp, p0.half, al, [s](const PairPlan& p, bool vec) {
     if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
     return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
-  });
+  }, pure);
 }
 
 int launch_staged(const StagedPlan& p0, void* stream) {
@@ -1038,10 +1128,17 @@ int launch_rows(const RowsPlan& p0, void* stream) {
   for (int m = 0; m < p0.NM; ++m) al = al && row_aligned(p0.msrc[m]);
   for (int x = 0; x < p0.NX; ++x) al = al && row_aligned(p0.xsrc[x]);
   for (int r = 0; r < p0.R; ++r) al = al && row_aligned(p0.dst[r]);
-  return split_launch(p0, p0.len, al, [s](const RowsPlan& p, bool vec) {
+  RowsPlan rp = p0;
+  rp.overlap = false;
+  bool pure = !p0.acc;  // no accumulate, and no destination that is also a source
+  for (int r = 0; r < p0.R && pure; ++r) {
+    for (int m = 0; m < p0.NM && pure; ++m) pure = !rows_overlap(p0.dst[r], p0.msrc[m], p0.len);
+    for (int x = 0; x < p0.NX && pure; ++x) pure = !rows_overlap(p0.dst[r], p0.xsrc[x], p0.len);
+  }
+  return split_launch(rp, p0.len, al, [s](const RowsPlan& p, bool vec) {
     if (p.acc) return vec ? launch_rows_r<true, true>(p, s) : launch_rows_r<true, false>(p, s);
     return vec ? launch_rows_r<false, true>(p, s) : launch_rows_r<false, false>(p, s);
-  });
+  }, pure);
 }
 
 }  // namespace xrs

@@ -50,10 +50,12 @@ struct PairPlan {
   RowRef src[kMaxSrc];
   RowRef dst[kMaxOut];
   int8_t pb[kMaxSrc];  // piggyback target output of source c's a-half, or -1
-  bool encode12;       // pb follows the 12+4 XORSet (source c = data c): hot kernel
+  bool encode_xs;      // whole Encode in one launch: source c = data c, and c's
+                       // a-half rides on output 1 + c % (P-1) (the XORSet)
   uint64_t half;       // H = size/2 bytes
   uint64_t n_stripes;
   uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_pair)
+  bool overlap;        // set by launch_pair: ragged end as one overlapping 16-B chunk
 };
 
 struct RowsPlan {
@@ -69,6 +71,7 @@ struct RowsPlan {
   uint64_t len;  // bytes per row
   uint64_t n_stripes;
   uint64_t off0, end;  // byte range [off0, end) of each row (set by launch_rows)
+  bool overlap;        // set by launch_rows: ragged end as one overlapping 16-B chunk
 };
 
 // "staged" kernel: the general Reconst (xrs.go:236-301) in one pass, each of
@@ -95,6 +98,7 @@ struct StagedPlan {
   uint64_t half;
   uint64_t n_stripes;
   uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_staged)
+  bool overlap;        // unused (in-place writes: the ragged end is its own launch)
 };
 
 // "update_rows" kernel: Update (xrs.go:324) where every stripe names its own
@@ -116,6 +120,7 @@ struct UpdRowsPlan {
   uint64_t half;
   uint64_t n_stripes;
   uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_update_rows)
+  bool overlap;        // unused (accumulates: the ragged end is its own launch)
 };
 
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.

@@ -112,14 +112,18 @@ def test_cpp_port_under_host_asan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.fixture(params=["staged", "staged_early", "staged_late", "stepwise"])
+@pytest.fixture(params=["staged", "staged_early", "staged_late", "staged_late_rt", "stepwise"])
 def reconst_mode(request, monkeypatch):
     monkeypatch.delenv("XRS_RECONST", raising=False)
     monkeypatch.delenv("XRS_STAGED_LATE", raising=False)
+    monkeypatch.delenv("XRS_STAGED_CT", raising=False)
     if request.param == "staged_early":
         monkeypatch.setenv("XRS_STAGED_LATE", "0")
-    elif request.param == "staged_late":
+    elif request.param == "staged_late":  # compile-time kernel where it applies
         monkeypatch.setenv("XRS_STAGED_LATE", "1")
+    elif request.param == "staged_late_rt":  # the runtime-count late kernel
+        monkeypatch.setenv("XRS_STAGED_LATE", "1")
+        monkeypatch.setenv("XRS_STAGED_CT", "0")
     elif request.param == "stepwise":
         monkeypatch.setenv("XRS_RECONST", "steps")
     return request.param
@@ -189,6 +193,33 @@ def test_reconst_every_loss_pattern(rng, reconst_mode, order):
             o.reconst(b, has, list(lost))
             for i in range(D + P):
                 assert np.array_equal(a[i], b[i]), (lost, order, i)
+
+
+@pytest.mark.parametrize("ct", ["1", "0"])
+@pytest.mark.parametrize("size,n", [(4096, 600), (1 << 20, 4), (4112, 520)])
+def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
+    """General Reconst of batches large enough for the bandwidth kernels
+    (compile-time staged kernel for lost data vects, XRS_STAGED_CT=0 the
+    runtime-count one), side effects included, every stripe vs the oracle."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("XRS_STAGED_CT", ct)
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    s = torch.cuda.current_stream().cuda_stream
+    for lost, need in (([0, 1], [0, 1]), ([0, 1, 2], [0, 1, 2]), ([0, 1, 2, 3], [0, 1, 2, 3]),
+                       ([4, 9], [9, 4]), ([2, 5, 11], [5]), ([1, 13], [1, 13]), ([3, 7, 8], [])):
+        h = host.copy()
+        h[:, lost] = 0x5A
+        has = [i for i in range(D + P) if i not in lost]
+        t = torch.from_numpy(h).cuda()
+        x.reconst_batched(t.data_ptr(), size, size, (D + P) * size, n, has, need, s)
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        for st in range(n):
+            w = [h[st, i].copy() for i in range(D + P)]
+            o.reconst(w, has, need)
+            assert np.array_equal(got[st], np.stack(w)), (lost, need, st)
 
 
 def test_codec_first_then_torch():

@@ -115,10 +115,11 @@ def main():
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)
-            for mode in ("late", "early", "steps"):
+            for mode in ("ct", "late", "early", "steps"):
                 # read per call by the library
                 os.environ["XRS_RECONST"] = mode
                 os.environ["XRS_STAGED_LATE"] = "0" if mode == "early" else "1"
+                os.environ["XRS_STAGED_CT"] = "1" if mode.startswith("ct") else "0"
                 for lost in (1, 2, 3, 4):
                     need = list(range(lost))
                     has = list(range(lost, D + P))
@@ -129,6 +130,7 @@ def main():
                     emit(f"reconst_{lost}_{mode}", size, n, secs, n * per, sh)
             os.environ.pop("XRS_RECONST", None)
             os.environ.pop("XRS_STAGED_LATE", None)
+            os.environ.pop("XRS_STAGED_CT", None)
             del t
     if "others" in cases:  # other (d, p): runtime-count kernels
         for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3)):
@@ -145,6 +147,23 @@ def main():
                 emit(f"reconst_one_{d}+{p}", size, n, secs,
                      n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
                 del t
+    if "multi_order" in cases:  # staged Reconst (compile-time kernel) in every block order
+        for size, n in ((4096, 65536), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            for order in ("", "0", "8", "32", "128", "512", "full"):
+                if order:
+                    os.environ["XRS_BLOCK_ORDER"] = order
+                else:
+                    os.environ.pop("XRS_BLOCK_ORDER", None)
+                for lost in (2, 3, 4):
+                    need, has = list(range(lost)), list(range(lost, D + P))
+                    secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has,
+                                                             need, s))
+                    emit(f"reconst_{lost}_order_{order or 'default'}", size, n, secs,
+                         n * (D + lost) * size, sh)
+            os.environ.pop("XRS_BLOCK_ORDER", None)
+            del t
     if "others_ab" in cases:  # other (d, p): compile-time shapes vs runtime-count kernels
         for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3), (14, 4), (10, 2)):
             xo = xrs_amd.XRS(d, p)

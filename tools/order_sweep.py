@@ -53,6 +53,8 @@ def main():
                                                          list(range(lo)), s)))
             continue
         shard, stripe = xrs_amd.batch_strides(size, D + P)
+        if os.environ.get("LAYOUT") == "packed":  # shards back to back at any size
+            shard, stripe = size, (D + P) * size
         buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
         base = buf.data_ptr()
         cases.append((f"encode_{size}", (D + P) * size * n, buf,

@@ -609,6 +609,116 @@ __global__ __launch_bounds__(kBlock) void staged_late_kernel(const StagedArgs<NL
   }
 }
 
+// Compile-time variant of the late-b kernel for the clean loss patterns of a
+// d = ND codec whose a-rows are exactly the ND survivors (lost data vects at
+// 12+4: na = 12, nb = 12 + surviving piggybacked parity past dpHas[:d]).
+// Every load is unconditional and every store comes after the loads of its
+// phase, so the waitcnt pass never has to assume a conditional memory op
+// is outstanding (the runtime-count kernels wait for vmcnt(0) at every
+// guarded load).  Phase A: ND a-row loads, lost a-halves, the retrieveRS and
+// re-piggyback XOR terms, the lost a-half stores.  Phase B: NB b-row loads,
+// retrieveRS XORs, the needed b-halves, then every b store.
+template <int ND, int NL, int W>
+__device__ __forceinline__ void abar_ct(uint32_t* acc, uint32_t mask, const uint32_t (&xa)[ND][W],
+                                        const uint32_t (&al)[NL][W]) {
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+    if ((mask >> j) & 1u)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[w] ^= xa[j][w];
+#pragma unroll
+  for (int q = 0; q < NL; ++q)
+    if ((mask >> (kStSrc + q)) & 1u)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[w] ^= al[q][w];
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2 gu32x2;
+
+// W dwords per lane (4: dwordx4, 2: dwordx2), nontemporal, any alignment.
+template <int W>
+__device__ __forceinline__ void ldw(uint32_t* v, uint64_t addr) {
+  if constexpr (W == 4) {
+    ld<true>(v, addr, 16);
+  } else {
+    const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const gu32x2*>(addr));
+    v[0] = t.x;
+    v[1] = t.y;
+  }
+}
+template <int W>
+__device__ __forceinline__ void stw(const uint32_t* v, uint64_t addr) {
+  if constexpr (W == 4) {
+    st<true>(v, addr, 16);
+  } else {
+    u32x2 t;
+    t.x = v[0];
+    t.y = v[1];
+    __builtin_nontemporal_store(t, reinterpret_cast<gu32x2*>(addr));
+  }
+}
+
+template <int ND, int NB, int NL, int NN, int W>
+__global__ __launch_bounds__(kBlock) void staged_ct_kernel(const StagedArgs<NL, NN, true> a) {
+  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
+  if (gid >= a.total) return;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+
+  uint32_t xa[ND][W], al[NL][W], rx[kStOut][W], ob[NN][W];
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int m = 0; m < ND; ++m) ldw<W>(xa[m], row_addr(a.asrc[m], stripe, off));
+  __builtin_amdgcn_s_setprio(0);
+  // Stage 1: lost a-halves (xrs.go:247-262).
+#pragma unroll
+  for (int q = 0; q < NL; ++q)
+#pragma unroll
+    for (int w = 0; w < W; ++w) al[q][w] = 0u;
+#pragma unroll
+  for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+  if constexpr (ND & 1) rows_mac1<NL, W>(al, a.at[ND - 1], xa[ND - 1]);
+  // XOR terms of stage 2 (retrieveRS, xrs.go:305-320) and stage 4
+  // (re-piggyback, :281-297), from the a-rows and the rebuilt a-halves.
+#pragma unroll
+  for (int r = 0; r < kStOut; ++r) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) rx[r][w] = 0u;
+    if (r < a.nr) abar_ct<ND, NL, W>(rx[r], a.rmask[r], xa, al);
+  }
+#pragma unroll
+  for (int u = 0; u < NN; ++u) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) ob[u][w] = 0u;
+    if (a.nmask[u]) abar_ct<ND, NL, W>(ob[u], a.nmask[u], xa, al);
+  }
+#pragma unroll
+  for (int q = 0; q < NL; ++q) stw<W>(al[q], row_addr(a.adst[q], stripe, off));
+
+  uint32_t xb[NB][W];
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int r = 0; r < kStOut; ++r)
+      if (r < a.nr && a.rb[r] == m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) xb[m][w] ^= rx[r][w];
+  // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
+#pragma unroll
+  for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+  if constexpr (ND & 1) rows_mac1<NN, W>(ob, a.bt[ND - 1], xb[ND - 1]);
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+    if ((a.bstore >> m) & 1u) stw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+#pragma unroll
+  for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
+}
+
 // ============================================================ update_rows kernel
 // Update with a per-stripe data row (xrs_plan.h UpdRowsPlan).  The row's
 // coefficient tables are read from the kernel arguments with a per-lane index
@@ -777,6 +887,25 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   // (A compile-time survivor count, ND = 12, let the scheduler hoist the
   // b-row loads: 225-232 VGPRs plus scratch, also with a sched_barrier
   // between the a- and b-phases.  Runtime nd only.)
+  if constexpr (VEC && NL == NN && NL >= 2) {
+    // Compile-time counts for 12+4 losses of data vects (na = nd = 12,
+    // nb = 12..14); XRS_STAGED_CT=0 keeps the runtime-count kernel (A/B).
+    const char* cv = std::getenv("XRS_STAGED_CT");
+    const bool ct = late && p.nd == 12 && p.na == 12 && p.nl == NL && p.nn == NN &&
+                    p.nb >= 12 && p.nb <= 14 && !(cv && cv[0] == '0');
+    if (ct) {
+      // (8 bytes per lane, twice the lanes at 56-70 VGPRs: 2-10% slower,
+      // profiles/r02_multi2.log.)
+      const dim3 g(static_cast<unsigned>(blocks));
+      if (p.nb == 12)
+        hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
+      else if (p.nb == 13)
+        hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
+      else
+        hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if (late)
     hipLaunchKernelGGL((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, stream, a);
@@ -993,7 +1122,12 @@ int launch_reconst_one_ct(const RowsPlan& p, hipStream_t s, Shape2<NMs, NXs>...)
 template <int R, bool ACC, bool VEC>
 int launch_rows_c(const RowsPlan& p, hipStream_t s) {
   if constexpr (R == 2 && !ACC && VEC) {  // (the byte path of these shapes would use scratch)
-    if (!std::getenv("XRS_ROWS_DYN")) {
+    // More than 22 rows in a 1024-thread block (rows of >= 256 KiB) would
+    // spill (128 VGPRs at most); those run the runtime-count kernel
+    // (20+4 ReconstOne @ 1 MiB: 0.66 compile-time with scratch, 0.76 runtime;
+    // profiles/r02_others_ab.log).
+    const bool fits = p.len < (256u << 10) || p.NM + p.NX <= 22;
+    if (fits && !std::getenv("XRS_ROWS_DYN")) {
       const int rc = launch_reconst_one_ct<VEC>(
           p, s, Shape2<12, 4>{},                     // 12+4
           Shape2<4, 4>{}, Shape2<6, 3>{},            // 4+2, 6+3

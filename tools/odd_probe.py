@@ -30,7 +30,9 @@ def timed(fn, reps=10):
     return a.elapsed_time(b) / reps / 1e3
 
 
-TAILS = ("overlap", "launch")  # XRS_TAIL: ragged end in the 16-B launch / its own launch
+# (env var, value) pairs A/B'd: the ragged end in the 16-B launch (default) or
+# its own launch; lanes padded so no wave spans two stripes.
+TAILS = {"overlap": {}, "launch": {"XRS_TAIL": "launch"}, "wave_align": {"XRS_WAVE_ALIGN": "1"}}
 
 
 def main():
@@ -47,11 +49,14 @@ def main():
                  lambda: x.reconst_one_batched(base, size, size, stripe, n, 3, s))):
             best = {}
             for rep in range(3):  # interleaved A/B rounds; best of each
-                for tail in TAILS:
-                    os.environ["XRS_TAIL"] = tail
+                for tail, env in TAILS.items():
+                    for k in ("XRS_TAIL", "XRS_WAVE_ALIGN"):
+                        os.environ.pop(k, None)
+                    os.environ.update(env)
                     secs = timed(fn)
                     best[tail] = min(best.get(tail, 1e9), secs)
-            os.environ.pop("XRS_TAIL", None)
+            for k in ("XRS_TAIL", "XRS_WAVE_ALIGN"):
+                os.environ.pop(k, None)
             print(json.dumps({"op": op, "vect_bytes": size, "base_off": base_off,
                               **{f"gbs_{t}": round(nbytes / best[t] / 1e9, 1) for t in TAILS}}),
                   flush=True)

@@ -36,6 +36,8 @@ __device__ __forceinline__ void st(u32x4 v, uint64_t a) {
 
 // One lane: 16 B at offset `off` of both halves of 12 source rows and 4 output
 // rows of one stripe.  XCD-aware order as in the product (K = 32).
+// chunks: lanes per stripe-half (>= ceil(half/16); rounded up to a multiple of
+// 64 = one wave never spans two stripes, the extra lanes exit).
 template <bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void enc_xor(uint64_t base, uint64_t shard, uint64_t half,
                                               uint64_t chunks, uint64_t total, uint32_t nblk) {
@@ -46,6 +48,7 @@ __global__ __launch_bounds__(256) void enc_xor(uint64_t base, uint64_t shard, ui
   if (gid >= total) return;
   const uint64_t stripe = gid / chunks;
   uint64_t off = (gid - stripe * chunks) * 16;
+  if (off >= half) return;               // wave-aligned padding lanes
   if (off > half - 16) off = half - 16;  // ragged end: overlapping last chunk
   const uint64_t s0 = base + stripe * 16 * shard;
   u32x4 a[12], bb[12];
@@ -64,8 +67,11 @@ __global__ __launch_bounds__(256) void enc_xor(uint64_t base, uint64_t shard, ui
 }
 
 template <bool NTL, bool NTS>
-double run(uint8_t* buf, uint64_t shard, uint64_t size, uint64_t n) {
-  const uint64_t half = size / 2, chunks = (half + 15) / 16, total = chunks * n;
+double run(uint8_t* buf, uint64_t shard, uint64_t size, uint64_t n, bool wave_align = false) {
+  const uint64_t half = size / 2;
+  uint64_t chunks = (half + 15) / 16;
+  if (wave_align) chunks = (chunks + 63) / 64 * 64;
+  const uint64_t total = chunks * n;
   const uint32_t nblk = (uint32_t)((total + 255) / 256);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -90,20 +96,19 @@ int main() {
   uint8_t* buf;
   CK(hipMalloc(&buf, budget + (1 << 20)));
   CK(hipMemset(buf, 0x3c, budget + (1 << 20)));
-  const uint64_t sizes[] = {4096, 4100, 4128, 4224, 1 << 20, (1 << 20) + 2, (1 << 20) + 32};
+  const uint64_t sizes[] = {4096, 4100, 4128, 4224, 6144, 8192, 8200, 1 << 20, (1 << 20) + 2};
   for (int rep = 0; rep < 2; ++rep)
-    for (uint64_t size : sizes) {
-      const uint64_t shard = size, n = budget / (16 * shard);
-      double g[4];
-      g[0] = run<true, true>(buf, shard, size, n);
-      g[1] = run<false, false>(buf, shard, size, n);
-      g[2] = run<true, false>(buf, shard, size, n);
-      g[3] = run<false, true>(buf, shard, size, n);
-      std::printf("{\"round\": %d, \"vect_bytes\": %llu, \"gbs_ntl_nts\": %.1f, \"gbs_plain\": %.1f, "
-                  "\"gbs_ntl_plainst\": %.1f, \"gbs_plainld_nts\": %.1f}\n",
-                  rep, (unsigned long long)size, g[0], g[1], g[2], g[3]);
-      std::fflush(stdout);
-    }
+    for (uint64_t size : sizes)
+      for (uint64_t shard : {size, (size + 15) / 16 * 16, (size + 127) / 128 * 128,
+                             (size + 4095) / 4096 * 4096}) {
+        const uint64_t n = budget / (16 * shard);
+        const double g0 = run<true, true>(buf, shard, size, n);
+        const double g1 = run<true, true>(buf, shard, size, n, true);
+        std::printf("{\"round\": %d, \"vect_bytes\": %llu, \"shard_stride\": %llu, "
+                    "\"gbs\": %.1f, \"gbs_wave_aligned\": %.1f}\n",
+                    rep, (unsigned long long)size, (unsigned long long)shard, g0, g1);
+        std::fflush(stdout);
+      }
   CK(hipFree(buf));
   return 0;
 }

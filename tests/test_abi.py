@@ -146,3 +146,13 @@ def test_single_hip_runtime():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_batch_strides_recommendation():
+    """xrs_batch_strides (codec.cpp): shards back to back below 4 MiB, odd
+    sizes back to back below 32 KiB, 16-rounded from there, a 4 KiB + 256 B
+    pad from 4 MiB up (profiles/r02_stride_probe.log, r01_order_ab.log)."""
+    cases = {4096: 4096, 4100: 4100, 2: 2, 1026: 1026, 65536: 65536, 65538: 65552,
+             1 << 20: 1 << 20, (1 << 20) + 2: (1 << 20) + 16, 8 << 20: (8 << 20) + 4352}
+    for size, shard in cases.items():
+        assert xrs_amd.batch_strides(size, 16) == (shard, 16 * shard), size

@@ -495,7 +495,7 @@ def test_golden_codecs_gpu(golden_codecs, cuda, d, p, S):
     assert np.array_equal(np.stack(par), g[k + "rp_out"])
 
 
-@pytest.mark.parametrize("tail", ["overlap", "launch", "wave_align"])
+@pytest.mark.parametrize("tail", ["overlap", "launch"])
 @pytest.mark.parametrize("size,n", [(4100, 300), (1048578, 3), (34, 500), (18, 200), (4126, 100),
                                     (4098, 100), (65538, 20)])
 def test_ragged_sizes_encode_reconst_one_vs_oracle(cuda, rng, monkeypatch, tail, size, n):
@@ -506,8 +506,6 @@ def test_ragged_sizes_encode_reconst_one_vs_oracle(cuda, rng, monkeypatch, tail,
     shards untouched (padded layout, odd strides)."""
     if tail == "launch":
         monkeypatch.setenv("XRS_TAIL", "launch")
-    elif tail == "wave_align":
-        monkeypatch.setenv("XRS_WAVE_ALIGN", "1")
     o = OracleXRS(D, P)
     x = xrs_amd.XRS(D, P)
     for shard_stride in (size, size + 7):

@@ -31,8 +31,9 @@ def timed(fn, reps=10):
 
 
 # (env var, value) pairs A/B'd: the ragged end in the 16-B launch (default) or
-# its own launch; lanes padded so no wave spans two stripes.
-TAILS = {"overlap": {}, "launch": {"XRS_TAIL": "launch"}, "wave_align": {"XRS_WAVE_ALIGN": "1"}}
+# its own launch.  (Padding each stripe's lanes to whole waves, so no wave
+# spans two stripes, measured 0-10% slower: profiles/r02_odd_probe2.log.)
+TAILS = {"overlap": {}, "launch": {"XRS_TAIL": "launch"}}
 
 
 def main():
@@ -50,13 +51,11 @@ def main():
             best = {}
             for rep in range(3):  # interleaved A/B rounds; best of each
                 for tail, env in TAILS.items():
-                    for k in ("XRS_TAIL", "XRS_WAVE_ALIGN"):
-                        os.environ.pop(k, None)
+                    os.environ.pop("XRS_TAIL", None)
                     os.environ.update(env)
                     secs = timed(fn)
                     best[tail] = min(best.get(tail, 1e9), secs)
-            for k in ("XRS_TAIL", "XRS_WAVE_ALIGN"):
-                os.environ.pop(k, None)
+            os.environ.pop("XRS_TAIL", None)
             print(json.dumps({"op": op, "vect_bytes": size, "base_off": base_off,
                               **{f"gbs_{t}": round(nbytes / best[t] / 1e9, 1) for t in TAILS}}),
                   flush=True)

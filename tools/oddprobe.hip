@@ -96,17 +96,30 @@ int main() {
   uint8_t* buf;
   CK(hipMalloc(&buf, budget + (1 << 20)));
   CK(hipMemset(buf, 0x3c, budget + (1 << 20)));
-  const uint64_t sizes[] = {4096, 4100, 4128, 4224, 6144, 8192, 8200, 1 << 20, (1 << 20) + 2};
+  // Shard-stride sweep: vect size -> strides tried (stripe stride = 16 shards).
+  struct Case {
+    uint64_t size;
+    int nstrides;
+    uint64_t strides[14];
+  };
+  const Case cases[] = {
+      {4096, 10, {4096, 4112, 4128, 4160, 4224, 4352, 4608, 5120, 6144, 8192}},
+      {4100, 14, {4100, 4104, 4108, 4112, 4116, 4120, 4128, 4160, 4224, 4352, 4608, 5120, 6144, 8192}},
+      {2052, 8, {2052, 2056, 2064, 2080, 2112, 2176, 2304, 4096}},
+      {65538, 8, {65538, 65552, 65568, 65600, 65664, 65792, 66048, 69632}},
+      {1 << 20, 9, {1 << 20, (1 << 20) + 16, (1 << 20) + 32, (1 << 20) + 64, (1 << 20) + 128,
+                    (1 << 20) + 256, (1 << 20) + 1024, (1 << 20) + 4096, (1 << 20) + 4352}},
+      {(1 << 20) + 2, 9, {(1 << 20) + 2, (1 << 20) + 16, (1 << 20) + 32, (1 << 20) + 64,
+                          (1 << 20) + 128, (1 << 20) + 256, (1 << 20) + 1024, (1 << 20) + 4096,
+                          (1 << 20) + 4352}},
+  };
   for (int rep = 0; rep < 2; ++rep)
-    for (uint64_t size : sizes)
-      for (uint64_t shard : {size, (size + 15) / 16 * 16, (size + 127) / 128 * 128,
-                             (size + 4095) / 4096 * 4096}) {
-        const uint64_t n = budget / (16 * shard);
-        const double g0 = run<true, true>(buf, shard, size, n);
-        const double g1 = run<true, true>(buf, shard, size, n, true);
-        std::printf("{\"round\": %d, \"vect_bytes\": %llu, \"shard_stride\": %llu, "
-                    "\"gbs\": %.1f, \"gbs_wave_aligned\": %.1f}\n",
-                    rep, (unsigned long long)size, (unsigned long long)shard, g0, g1);
+    for (const Case& c : cases)
+      for (int i = 0; i < c.nstrides; ++i) {
+        const uint64_t shard = c.strides[i], n = budget / (16 * shard);
+        const double g0 = run<true, true>(buf, shard, c.size, n);
+        std::printf("{\"round\": %d, \"vect_bytes\": %llu, \"shard_stride\": %llu, \"gbs\": %.1f}\n",
+                    rep, (unsigned long long)c.size, (unsigned long long)shard, g0);
         std::fflush(stdout);
       }
   CK(hipFree(buf));

@@ -991,9 +991,15 @@ int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* s
   if (!shard_stride || !stripe_stride || n_shards < 1) return XRS_ERR_INVALID_ARG;
   // With the XCD-aware block order (kernels.hip) back-to-back shards stream
   // as fast as padded ones below 4 MiB; 8 MiB Encode still gains ~3% from a
-  // 4 KiB + 256 B pad (profiles/r01_order_ab.log).
+  // 4 KiB + 256 B pad (profiles/r01_order_ab.log).  A vect size that is not a
+  // multiple of 16 stays back to back below 32 KiB (the kernels take any
+  // alignment) and is rounded up to 16 from there: the rate follows the
+  // stride through the HBM address mapping, and a 16-rounded stride of
+  // 4,100-B vects (4,112) ran Encode / ReconstOne 17% / 8% slower than the
+  // back-to-back 4,100, while at 64 KiB + 2 and 1 MiB + 2 the rounded
+  // stride is 4-5% faster (tools/stride_probe.py, profiles/r02_stride_probe.log).
   const size_t pad = size >= (4u << 20) ? 4096 + 256 : 0;
-  const size_t s = (size + 15) / 16 * 16 + pad;
+  const size_t s = (size % 16 && size < (32u << 10)) ? size : (size + 15) / 16 * 16 + pad;
   *shard_stride = s;
   *stripe_stride = s * static_cast<size_t>(n_shards);
   return XRS_OK;

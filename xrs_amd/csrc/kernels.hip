@@ -150,7 +150,6 @@ struct PairArgs {
   uint64_t total;   // n_stripes * chunks
   uint64_t off0;    // first byte of each half this launch covers
   uint64_t last;    // ragged end: the last chunk starts here (overlap), else ~0
-  uint64_t limit;   // lanes whose chunk starts at or past this exit (wave padding)
 };
 
 template <int P, int W>
@@ -220,7 +219,6 @@ __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off >= a.limit) return;       // padding lanes of a wave-aligned stripe
   if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
@@ -313,8 +311,7 @@ struct RowsArgs {
   uint64_t chunks;
   uint64_t total;
   uint64_t off0;
-  uint64_t last;   // ragged end: the last chunk starts here (overlap), else ~0
-  uint64_t limit;  // lanes whose chunk starts at or past this exit (wave padding)
+  uint64_t last;  // ragged end: the last chunk starts here (overlap), else ~0
 };
 
 template <int R, int W>
@@ -361,7 +358,6 @@ __global__ __launch_bounds__(BS) void rows_kernel(const RowsArgs<R, NM, NX, VEC>
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off >= a.limit) return;       // padding lanes of a wave-aligned stripe
   if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
   const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
 
@@ -828,15 +824,6 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks, int
   return o;
 }
 
-// XRS_WAVE_ALIGN=1 (A/B experiments): pad the lanes of each stripe to a
-// multiple of 64, so no wave spans two stripes (the padding lanes exit).
-bool wave_align(bool vec, uint64_t* chunks) {
-  const char* e = std::getenv("XRS_WAVE_ALIGN");
-  if (!vec || !e || e[0] != '1' || *chunks % 64 == 0) return false;
-  *chunks = (*chunks + 63) / 64 * 64;
-  return true;
-}
-
 // Threads per block for a kernel family: `def`, or the env override when it
 // names a size this build instantiates for that family.
 int env_block(const char* var, int def) {
@@ -1003,7 +990,6 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   a.off0 = p.off0;
   a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
   a.last = (VEC && p.overlap) ? p.end - 16 : ~uint64_t(0);
-  a.limit = wave_align(VEC, &a.chunks) ? p.end : ~uint64_t(0);
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   // 128-thread blocks for the 16-byte kernels on halves up to 4 KiB (Encode
@@ -1096,7 +1082,6 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   a.off0 = p.off0;
   a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
   a.last = (VEC && p.overlap) ? p.end - 16 : ~uint64_t(0);
-  a.limit = wave_align(VEC, &a.chunks) ? p.end : ~uint64_t(0);
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   // 1024-thread blocks for rows of >= 256 KiB (ReconstOne at 1 MiB vects:

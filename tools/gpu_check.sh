@@ -16,17 +16,19 @@ run() {  # name seconds cmd...
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
 if [[ $STEPS == *pytest* ]]; then
-  run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider ${PYTEST_ARGS:-}
+  run pytest_gpu 1200 python -u -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider \
+      --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
   rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 if [[ $STEPS == *smoke* ]]; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
 if [[ $STEPS == *bench* ]]; then
-  run bench 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 8} || exit $?
+  run bench 600 python bench.py ${BENCH_ARGS:-} || exit $?
 fi
 if [[ $STEPS == *prof* ]]; then
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+      python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 \
+      --xgmi-stripes 0 || exit $?
 fi
 exit 0

@@ -147,6 +147,23 @@ def main():
                 emit(f"reconst_one_{d}+{p}", size, n, secs,
                      n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
                 del t
+    if "multi_bs" in cases:  # staged Reconst (compile-time kernel) at every block size
+        for size, n in ((4096, 65536), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(2):
+                for bs in ("128", "256", "512", "1024"):
+                    os.environ["XRS_STAGED_BLOCK"] = bs
+                    for lost in (2, 3, 4):
+                        need, has = list(range(lost)), list(range(lost, D + P))
+                        secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n,
+                                                                 has, need, s))
+                        res[(bs, lost)] = min(res.get((bs, lost), 1e9), secs)
+            os.environ.pop("XRS_STAGED_BLOCK", None)
+            for (bs, lost), secs in sorted(res.items()):
+                emit(f"reconst_{lost}_block_{bs}", size, n, secs, n * (D + lost) * size, sh)
+            del t
     if "multi_order" in cases:  # staged Reconst (compile-time kernel) in every block order
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

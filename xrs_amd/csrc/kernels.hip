@@ -659,9 +659,10 @@ __device__ __forceinline__ void stw(const uint32_t* v, uint64_t addr) {
   }
 }
 
-template <int ND, int NB, int NL, int NN, int W>
-__global__ __launch_bounds__(kBlock) void staged_ct_kernel(const StagedArgs<NL, NN, true> a) {
-  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
+template <int ND, int NB, int NL, int NN, int BS>
+__global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, true> a) {
+  constexpr int W = 4;
+  const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
@@ -833,6 +834,21 @@ int env_block(const char* var, int def) {
   return (v == 256 || v == def) ? v : def;
 }
 
+template <int NL, int NN, int BS>
+int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+  const uint64_t blocks = (a.total + BS - 1) / BS;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kStaged, true, p.half, blocks, BS);
+  const dim3 g(static_cast<unsigned>(blocks));
+  if (p.nb == 12)
+    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+  else if (p.nb == 13)
+    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+  else
+    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 template <int NL, int NN, bool VEC>
 int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   StagedArgs<NL, NN, VEC> a;
@@ -895,15 +911,9 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
                     p.nb >= 12 && p.nb <= 14 && !(cv && cv[0] == '0');
     if (ct) {
       // (8 bytes per lane, twice the lanes at 56-70 VGPRs: 2-10% slower,
-      // profiles/r02_multi2.log.)
-      const dim3 g(static_cast<unsigned>(blocks));
-      if (p.nb == 12)
-        hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
-      else if (p.nb == 13)
-        hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
-      else
-        hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, 4>), g, dim3(kBlock), 0, stream, a);
-      return static_cast<int>(hipGetLastError());
+      // profiles/r02_multi2.log; 128-, 512- and 1024-thread blocks: 0-7%
+      // slower at 4 KiB, within 1% at 1 MiB, profiles/r02_multi_bs.log.)
+      return launch_staged_ct_bs<NL, NN, kBlock>(a, p, stream);
     }
   }
   if (late)

@@ -465,9 +465,11 @@ def run_xgmi_child(args, device: int, ndev: int):
     cmd = [sys.executable, os.path.abspath(__file__), "--xgmi-child", str(device),
            "--xgmi-stripes", str(args.xgmi_stripes)]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env)
     except subprocess.TimeoutExpired:
-        return {"error": "timed out after 240 s"}
+        return {"error": "timed out after 150 s"}
+    except OSError as e:
+        return {"error": f"could not start the probe: {e}"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-800:]}

@@ -394,62 +394,76 @@ def host_e2e(R: Rank, args):
 
 def xgmi_repair(R: Rank, args):
     """Cross-GPU repair: rank 0 rebuilds data shard k of
-    1 MiB stripes whose odd-numbered shards live on the peer GPU, reading them
-    over xGMI (xrs_reconst_one_shards after xrs_enable_peer_access), and checks
-    the result bit for bit against the rebuild from all-local shards.
+    1 MiB stripes whose shards live on other GPUs, reading them over xGMI
+    (xrs_reconst_one_shards after xrs_enable_peer_access), and checks the
+    result bit for bit against the stored shard.  Two placements:
+      * "half":   the odd-numbered shards on the next GPU;
+      * "spread": shard i on GPU (device + i) mod (GPUs visible), i.e. a
+                  stripe spread over the node, 2 shards per GPU at 8 GPUs.
+    The rate is algorithmic bytes (9*S per stripe, xrs_test.go:565-572) over
+    the call, next to the same rebuild from all-local shards.
     Semantics: xrs.go:175-221."""
     torch, x, s = R.torch, R.x, R.stream
-    # XRS_XGMI_SELF=1 on a one-GPU box: the "peer" is the same device (every
+    dev, ndev = R.dev_index, R.ndev
+    # XRS_XGMI_SELF=1 on a one-GPU box: every "peer" is the same device (every
     # step but the xGMI reads themselves; tests/test_gpu_bench.py)
-    peer = (R.dev_index + 1) % R.ndev
-    if peer != R.dev_index:
-        rc = R.xrs_amd.lib().xrs_enable_peer_access(R.dev_index, peer)
+    for q in sorted({(dev + j) % ndev for j in range(1, D + P)} - {dev}):
+        rc = R.xrs_amd.lib().xrs_enable_peer_access(dev, q)
         if rc != 0:
-            return {"skipped": f"peer access {R.dev_index}->{peer} unavailable (code {rc})"}
+            return {"skipped": f"peer access {dev}->{q} unavailable (code {rc})"}
     n, size, k = args.xgmi_stripes, REC_S, 4
     col = n * size  # shard-major: shard i of stripe t at base + i*col + t*size
     local = R.random_bytes((D + P) * col, 0x961)
     x.encode_batched(local.data_ptr(), size, col, size, n, s)
     R.sync()
     expect = local[k * col:(k + 1) * col].clone()
-    remote = {i: local[i * col:(i + 1) * col].to(f"cuda:{peer}") for i in range(1, D + P, 2)}
-    torch.cuda.synchronize(peer)
-
-    def table():
-        return [remote[i].data_ptr() if i in remote else local.data_ptr() + i * col
-                for i in range(D + P)]
-
-    tab = table()
     a_need, b_need = x.get_need_vects(k)
     need = sorted(set([m for m in range(D) if m != k] + b_need + a_need))
-    on_peer = sum(1 for i in need if i in remote)
-    local[k * col:(k + 1) * col].zero_()
-    x.reconst_one_shards(tab, size, size, n, k, s)
-    R.sync()
-    exact = bool(torch.equal(local[k * col:(k + 1) * col], expect))
-    # same rebuild from all-local shards, for the rate next to it
-    lt = [local.data_ptr() + i * col for i in range(D + P)]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rates = {}
-    for name, t in (("mixed", tab), ("local", lt)):
+
+    def rate(table):
         for _ in range(2):
-            x.reconst_one_shards(t, size, size, n, k, s)
+            x.reconst_one_shards(table, size, size, n, k, s)
         reps = 10
         e0.record()
         for _ in range(reps):
-            x.reconst_one_shards(t, size, size, n, k, s)
+            x.reconst_one_shards(table, size, size, n, k, s)
         e1.record()
         R.sync()
-        ms = e0.elapsed_time(e1) / reps
-        rates[name] = round(n * 9 * size / (ms / 1e3) / 1e9, 1)
-    exact = exact and bool(torch.equal(local[k * col:(k + 1) * col], expect))
-    del remote, local, expect
+        return round(n * 9 * size / (e0.elapsed_time(e1) / reps / 1e3) / 1e9, 1)
+
+    placements = {"half": lambda i: dev if i % 2 == 0 else (dev + 1) % ndev,
+                  "spread": lambda i: (dev + i) % ndev}
+    out = {"device": dev, "gpus_visible": ndev, "stripes": n, "vect_bytes": size, "k": k,
+           "bytes_per_call": n * 9 * size, "layouts": {}}
+    exact_all = True
+    for name, place in placements.items():
+        copies = {i: local[i * col:(i + 1) * col].to(f"cuda:{place(i)}")
+                  for i in range(D + P) if i != k and (place(i) != dev or ndev == 1)}
+        for q in range(ndev):
+            torch.cuda.synchronize(q)
+        table = [copies[i].data_ptr() if i in copies else local.data_ptr() + i * col
+                 for i in range(D + P)]
+        local[k * col:(k + 1) * col].zero_()
+        x.reconst_one_shards(table, size, size, n, k, s)
+        R.sync()
+        exact = bool(torch.equal(local[k * col:(k + 1) * col], expect))
+        gbs = rate(table)
+        exact = exact and bool(torch.equal(local[k * col:(k + 1) * col], expect))
+        exact_all = exact_all and exact
+        out["layouts"][name] = {
+            "need_set_shards_remote": sum(1 for i in need if place(i) != dev),
+            "need_set_shards": len(need),
+            "gpus_read": sorted({place(i) for i in need}), "gbs_algorithmic": gbs,
+            "bitexact": exact}
+        del copies, table
+        torch.cuda.empty_cache()
+    out["gbs_all_local"] = rate([local.data_ptr() + i * col for i in range(D + P)])
+    out["gbs_algorithmic"] = out["layouts"]["half"]["gbs_algorithmic"]
+    out["xgmi_bitexact"] = exact_all
+    del local, expect
     torch.cuda.empty_cache()
-    return {"device": R.dev_index, "peer": peer, "stripes": n, "vect_bytes": size, "k": k,
-            "need_halves_on_peer": f"{on_peer} of {len(need)} need-set shards",
-            "xgmi_bitexact": exact,
-            "gbs_algorithmic": rates["mixed"], "gbs_all_local": rates["local"],
-            "bytes_per_call": n * 9 * size}
+    return out
 
 
 def run_xgmi_child(args, device: int, ndev: int):

@@ -659,7 +659,7 @@ __device__ __forceinline__ void stw(const uint32_t* v, uint64_t addr) {
   }
 }
 
-template <int ND, int NB, int NL, int NN, int BS>
+template <int ND, int NB, int NL, int NN, int BS, bool EARLY = false>
 __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, true> a) {
   constexpr int W = 4;
   const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
@@ -667,10 +667,14 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
 
-  uint32_t xa[ND][W], al[NL][W], rx[kStOut][W], ob[NN][W];
+  uint32_t xa[ND][W], al[NL][W], rx[kStOut][W], ob[NN][W], xb[NB][W];
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int m = 0; m < ND; ++m) ldw<W>(xa[m], row_addr(a.asrc[m], stripe, off));
+  if constexpr (EARLY) {  // every row's load in flight at once (one round trip)
+#pragma unroll
+    for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+  }
   __builtin_amdgcn_s_setprio(0);
   // Stage 1: lost a-halves (xrs.go:247-262).
 #pragma unroll
@@ -697,11 +701,12 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
 #pragma unroll
   for (int q = 0; q < NL; ++q) stw<W>(al[q], row_addr(a.adst[q], stripe, off));
 
-  uint32_t xb[NB][W];
-  __builtin_amdgcn_s_setprio(1);
+  if constexpr (!EARLY) {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
-  __builtin_amdgcn_s_setprio(0);
+    for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+    __builtin_amdgcn_s_setprio(0);
+  }
 #pragma unroll
   for (int m = 0; m < NB; ++m)
 #pragma unroll
@@ -834,18 +839,18 @@ int env_block(const char* var, int def) {
   return (v == 256 || v == def) ? v : def;
 }
 
-template <int NL, int NN, int BS>
+template <int NL, int NN, int BS, bool EARLY>
 int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + BS - 1) / BS;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, true, p.half, blocks, BS);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == 12)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
   else if (p.nb == 13)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
   else
-    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -913,7 +918,14 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // (8 bytes per lane, twice the lanes at 56-70 VGPRs: 2-10% slower,
       // profiles/r02_multi2.log; 128-, 512- and 1024-thread blocks: 0-7%
       // slower at 4 KiB, within 1% at 1 MiB, profiles/r02_multi_bs.log.)
-      return launch_staged_ct_bs<NL, NN, kBlock>(a, p, stream);
+      // Every row's load up front (one round trip, 144-161 VGPRs) on halves
+      // up to 4 KiB: +2.6-2.8% on 2-3 lost at 4 KiB vects; at 1 MiB the
+      // two-phase kernel is 1-5% faster (profiles/r02_multi3.log).
+      // XRS_STAGED_EARLY=0 / =1 forces either (A/B, tests).
+      const char* ev = std::getenv("XRS_STAGED_EARLY");
+      const bool early = (ev && *ev) ? ev[0] == '1' : p.half <= 4096;
+      if (early) return launch_staged_ct_bs<NL, NN, kBlock, true>(a, p, stream);
+      return launch_staged_ct_bs<NL, NN, kBlock, false>(a, p, stream);
     }
   }
   if (late)

@@ -563,3 +563,28 @@ def test_compile_time_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, 
             x.reconst_one_batched(t.data_ptr(), size, size, (d + p) * size, n, k, stream())
             torch.cuda.synchronize()
             assert np.array_equal(t.cpu().numpy(), ref), (size, k)
+
+
+@pytest.mark.parametrize("mode", ["ct", "dyn"])
+@pytest.mark.parametrize("size,n", [(4096, 40), (9000, 20), (8200, 9), (34, 30)])
+def test_replace_batched_every_n_vs_oracle(cuda, rng, monkeypatch, mode, size, n):
+    """Replace(n) for n = 1..8 at 12+4 (the reference's Replace benchmark
+    rows, xrs_test.go:627-680): compile-time source counts (halves > 4 KiB,
+    or n >= 5) and the runtime-count kernel (XRS_REPLACE_DYN), both
+    directions of the reference's test (zero -> data, data -> zero)."""
+    if mode == "dyn":
+        monkeypatch.setenv("XRS_REPLACE_DYN", "1")
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    for nrep in range(1, 9):
+        rows = [int(v) for v in rng.permutation(D)[:nrep]]
+        data = rng.integers(0, 256, size=(n, nrep, size), dtype=np.uint8)
+        par = rng.integers(0, 256, size=(n, P, size), dtype=np.uint8)
+        td, tp = to_dev(data, cuda), to_dev(par, cuda)
+        x.replace_batched(td.data_ptr(), size, nrep * size, rows, size, tp.data_ptr(), size,
+                          P * size, n, stream())
+        torch.cuda.synchronize()
+        ref = par.copy()
+        for st in range(n):
+            pv = [ref[st, q] for q in range(P)]
+            o.replace([data[st, i].copy() for i in range(nrep)], rows, pv)
+        assert np.array_equal(tp.cpu().numpy(), ref), (nrep, rows)

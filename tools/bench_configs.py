@@ -149,6 +149,27 @@ def main():
                 emit(f"reconst_one_{d}+{p}", size, n, secs,
                      n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
                 del t
+    if "replace_ab" in cases:  # Replace(n): compile-time vs runtime source count
+        for size, n in ((4096, 65536), (8 << 20, 32)):
+            t, sh, st = batch(size, n, dev, 7)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            par = t.data_ptr() + D * sh
+            res = {}
+            for rnd in range(2):
+                for mode in ("ct", "dyn"):
+                    if mode == "dyn":
+                        os.environ["XRS_REPLACE_DYN"] = "1"
+                    else:
+                        os.environ.pop("XRS_REPLACE_DYN", None)
+                    for nrep in range(1, 9):
+                        rows = list(range(nrep))
+                        secs = timed(lambda i: x.replace_batched(t.data_ptr(), sh, st, rows, size,
+                                                                 par, sh, st, n, s))
+                        res[(mode, nrep)] = min(res.get((mode, nrep), 1e9), secs)
+            os.environ.pop("XRS_REPLACE_DYN", None)
+            for (mode, nrep), secs in sorted(res.items()):
+                emit(f"replace_{nrep}_{mode}", size, n, secs, n * (nrep + 2 * P) * size, sh)
+            del t
     if "multi_bs" in cases:  # staged Reconst (compile-time kernel) at every block size
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

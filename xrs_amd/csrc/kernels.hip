@@ -1062,11 +1062,30 @@ int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int
   return rc;
 }
 
+// Compile-time source counts of an accumulating launch with four outputs:
+// Replace(n) at p = 4, n = 1..8 (the reference's Replace benchmark,
+// xrs_test.go:627-680).
+template <bool VEC, int... Cs>
+int launch_replace_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int, Cs...>) {
+  int rc = -1;
+  (void)((p.C == Cs && (rc = launch_pair_t<4, Cs, true, VEC>(p, s), true)) || ...);
+  return rc;
+}
+
 template <int P, bool ACC, bool VEC>
 int launch_pair_c(const PairPlan& p, hipStream_t s) {
   if constexpr (!ACC && VEC && P >= 2) {
     if (p.encode_xs && !std::getenv("XRS_ENCODE_DYN")) {
       const int rc = launch_encode_ct<P, VEC>(p, s, typename EncodeShapes<P>::type{});
+      if (rc != -1) return rc;
+    }
+  }
+  if constexpr (ACC && VEC && P == 4) {
+    // Compile-time Replace(n): +0.5-2% at 8 MiB for every n and +2-4% at
+    // 4 KiB for n >= 5; at 4 KiB with n <= 4 the runtime kernel is as fast
+    // or up to 4% faster (profiles/r02_replace_ab.log).
+    if ((p.half > 4096 || p.C >= 5) && !std::getenv("XRS_REPLACE_DYN")) {
+      const int rc = launch_replace_ct<VEC>(p, s, std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 7, 8>{});
       if (rc != -1) return rc;
     }
   }

@@ -350,7 +350,7 @@ def config5(R: Rank, args):
                         "frac_per_gpu": round(rec_bytes * steps / rec_t / 1e9 / HBM_PEAK_GBS, 4)},
         "gibps": round(world_bytes(enc_bytes + rec_bytes) * steps / (enc_t + rec_t) / GIB, 1),
         "roundtrip_ok_rank0": ok,
-    }, ok
+    }
 
 
 def host_e2e(R: Rank, args):
@@ -520,7 +520,7 @@ def run_rank(args, w):
 
     c5 = None
     if args.config5_stripes > 0:
-        c5, _ = config5(R, args)
+        c5 = config5(R, args)
     he = host_e2e(R, args) if args.host_mib > 0 else None
     xg = None
     if args.xgmi_stripes > 0:

@@ -331,6 +331,7 @@ def config5(R: Rank, args):
     x.reconst_one_batched(base, REC_S, shard, stripe, n, k, s)
     R.sync()
     ok = bool(torch.equal(view, saved))
+    oks = [v > 0.5 for v in xdist.gather_seconds(1.0 if ok else 0.0, R.tdev)]  # every rank's check
     del buf, view, saved
     torch.cuda.empty_cache()
     enc_bytes, rec_bytes = n * (D + P) * REC_S, n * 9 * REC_S
@@ -349,7 +350,7 @@ def config5(R: Rank, args):
                         "gibps": round(world_bytes(rec_bytes) * steps / rec_t / GIB, 1),
                         "frac_per_gpu": round(rec_bytes * steps / rec_t / 1e9 / HBM_PEAK_GBS, 4)},
         "gibps": round(world_bytes(enc_bytes + rec_bytes) * steps / (enc_t + rec_t) / GIB, 1),
-        "roundtrip_ok_rank0": ok,
+        "roundtrip_ok": all(oks), "roundtrip_ok_ranks": oks,
     }
 
 

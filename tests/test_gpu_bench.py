@@ -42,7 +42,7 @@ def test_bench_one_gpu_contract():
     assert j["roofline"]["bound"] == "hbm" and 0 < j["roofline"]["frac"] < 1
     assert set(j["kernels"]) == {"encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m"}
     c5 = j["config5"]
-    assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok_rank0"]
+    assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok"]
     assert len(c5["encode"]["rank_seconds"]) == 1 and c5["gibps"] > 0
     assert set(j["host_e2e"]) >= {"encode_4k", "reconst_one_1m"}
     xg = j["xgmi_repair"]
@@ -76,7 +76,8 @@ def test_bench_two_ranks_contract():
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert len(j["rank_seconds"]) == 2 and min(j["rank_seconds"]) > 0
     assert abs(j["ms_per_step"] * j["steps"] / 1e3 - max(j["rank_seconds"])) < 1e-3
-    assert j["config5"]["stripes_total"] == 128 and j["config5"]["roundtrip_ok_rank0"]
+    c5 = j["config5"]
+    assert c5["stripes_total"] == 128 and c5["roundtrip_ok"] and len(c5["roundtrip_ok_ranks"]) == 2
     assert len(j["config5"]["reconst_one"]["rank_seconds"]) == 2
     assert len(j["host_e2e"]["encode_4k"]["rank_gibps"]) == 2
 

@@ -22,7 +22,8 @@ Multi-GPU (xrs_amd/dist.py): one process per GPU.  Under torchrun the ranks
 come from WORLD_SIZE (which must equal --gpus); `python bench.py --gpus N`
 without a launcher starts the N rank processes itself before any GPU call.
 Each rank owns its own batch (weak scaling, no collective on the data path;
-the barrier and the per-rank time gather only bracket the timed regions).
+the barrier and the per-rank time gather only bracket the timed regions, over
+gloo by default: no shard byte crosses ranks, so RCCL has nothing to carry).
 
 After the headline timed region, the same line carries:
   * "config5": BASELINE config 5, Encode + ReconstOne of --config5-stripes
@@ -498,7 +499,11 @@ def xgmi_child(args) -> int:
 
 
 def run_rank(args, w):
-    backend = os.environ.get("XRS_DIST_BACKEND", "nccl")
+    # The bracket around a timed region is a host barrier plus a gather of
+    # per-rank times: no byte of shard data crosses ranks, so no RCCL
+    # communicator is needed (gloo over 127.0.0.1).  XRS_DIST_BACKEND=nccl
+    # runs the same bracket over RCCL instead.
+    backend = os.environ.get("XRS_DIST_BACKEND", "gloo")
     R = Rank(w, backend)
     launches, step_bytes, rank_seconds, kernels, strides = headline(R, args)
     elapsed_max = max(rank_seconds)

@@ -1,7 +1,7 @@
 """GPU tests of bench.py's driver contract: one JSON line with the required
 keys, at N=1 and at N=2 (two ranks through torch.distributed.run; on the
-one-GPU box they share cuda:0 over gloo, as XRS_DIST_BACKEND=gloo selects —
-the driver's multi-GPU runs use nccl, one rank per GPU)."""
+one-GPU box they share cuda:0; the bracket runs over gloo, bench.py's default
+(RCCL refuses two ranks on one device, so XRS_DIST_BACKEND=nccl needs two GPUs))."""
 import json
 import os
 import socket
@@ -64,7 +64,7 @@ def test_bench_xgmi_child_self_peer():
 
 
 def test_bench_two_ranks_contract():
-    env = dict(os.environ, XRS_DIST_BACKEND="gloo")
+    env = dict(os.environ)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
@@ -87,7 +87,6 @@ def test_bench_self_launch_two_ranks():
     form the driver may use); on a one-GPU box they share cuda:0 over gloo."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    env["XRS_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]

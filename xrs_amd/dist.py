@@ -16,8 +16,10 @@ CPU, so what the 8-GPU run executes is what the CPU tests cover:
   * `timed_steps` / `timed_region` -- warmup, barrier + sync on both sides of
     exactly K steps, every rank's elapsed time gathered (max = the job time).
 
-Works with any torch.distributed backend: "nccl" (RCCL over xGMI) on the GPU
-box, "gloo" in the CPU tests and in one-card rehearsals.
+Works with any torch.distributed backend.  bench.py uses "gloo" by default:
+the bracket is a host barrier and a gather of a few floats, no shard byte
+crosses ranks, so an RCCL communicator would carry nothing ("nccl" still
+works, XRS_DIST_BACKEND=nccl).
 """
 from __future__ import annotations
 

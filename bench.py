@@ -308,9 +308,16 @@ def config5(R: Rank, args):
     xrs_test.go:476-480 (1 MiB Encode), xrs.go:175-221 (ReconstOne)."""
     torch, x, s = R.torch, R.x, R.stream
     w = R.w
-    total = args.config5_stripes * w.world
-    first, n = xdist.stripe_range(total, w.rank, w.world)
     shard, stripe = R.xrs_amd.batch_strides(REC_S, D + P)
+    # Every rank runs the same count: the requested one, or what the
+    # emptiest GPU's free HBM holds (minus 4 GiB), agreed over the ranks.
+    free, _ = torch.cuda.mem_get_info()
+    fits = max(0, (free - (4 << 30)) // stripe)
+    per_rank = int(min(xdist.gather_seconds(float(min(args.config5_stripes, fits)), R.tdev)))
+    if per_rank < 1:
+        return {"skipped": f"no room for one 16 MiB stripe ({free / GIB:.1f} GiB free)"}
+    total = per_rank * w.world
+    first, n = xdist.stripe_range(total, w.rank, w.world)
     t0 = time.perf_counter()
     buf = R.random_bytes(n * stripe, 0xC05 + first)
     base = buf.data_ptr()
@@ -342,7 +349,7 @@ def config5(R: Rank, args):
     return {
         "workload": (f"12+4 @ 1 MiB: {total} stripes ({total * (D + P) * REC_S / 2**40:.3f} TiB) "
                      f"split {n} per GPU over {w.world} GPU(s), no collective"),
-        "stripes_total": total, "stripes_per_rank": n,
+        "stripes_total": total, "stripes_per_rank": n, "stripes_requested": args.config5_stripes,
         "steps": steps,
         "encode": {"rank_seconds": [round(v, 6) for v in enc_sec],
                    "gibps": round(world_bytes(enc_bytes) * steps / enc_t / GIB, 1),

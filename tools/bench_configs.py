@@ -188,7 +188,11 @@ def main():
                 emit(f"reconst_{lost}_block_{bs}", size, n, secs, n * (D + lost) * size, sh)
             del t
     if "multi_order" in cases:  # staged Reconst (compile-time kernel) in every block order
-        for size, n in ((4096, 65536), (1 << 20, 256)):
+        sizes = ((4096, 65536), (1 << 20, 256))
+        if os.environ.get("MULTI_SIZES"):  # e.g. MULTI_SIZES=1048576
+            sizes = tuple((int(v), (4 << 30) // (16 * int(v))) for v in
+                          os.environ["MULTI_SIZES"].split(","))
+        for size, n in sizes:
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)
             for order in ("", "0", "8", "32", "128", "512", "full"):

@@ -919,11 +919,12 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // profiles/r02_multi2.log; 128-, 512- and 1024-thread blocks: 0-7%
       // slower at 4 KiB, within 1% at 1 MiB, profiles/r02_multi_bs.log.)
       // Every row's load up front (one round trip, 144-161 VGPRs) on halves
-      // up to 4 KiB: +2.6-2.8% on 2-3 lost at 4 KiB vects; at 1 MiB the
-      // two-phase kernel is 1-5% faster (profiles/r02_multi3.log).
+      // under 256 KiB: +2.6-2.8% on 2-3 lost at 4 KiB vects, +1-2.6% at
+      // 256 KiB; at 1 MiB the two-phase kernel is 1-5% faster
+      // (profiles/r02_multi3.log, r02_multi_order_e{0,1}.log).
       // XRS_STAGED_EARLY=0 / =1 forces either (A/B, tests).
       const char* ev = std::getenv("XRS_STAGED_EARLY");
-      const bool early = (ev && *ev) ? ev[0] == '1' : p.half <= 4096;
+      const bool early = (ev && *ev) ? ev[0] == '1' : p.half < (256u << 10);
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, true>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, false>(a, p, stream);
     }

@@ -408,6 +408,42 @@ def test_full_size_encode_erase_reconst(cuda, size, n):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("size,n", [(4096, 65536), (1 << 20, 512)])
+def test_full_size_multi_loss_side_effects(cuda, size, n):
+    """General Reconst (xrs.go:236-301) on full-size batches (4 / 8 GiB), the
+    loss patterns of the reference's Reconst benchmark (lost data[:i]) and
+    mixed data + parity losses, need = lost.  Without an oracle at this
+    size, the expected buffers follow from the reference's semantics: every
+    lost vect comes back whole, and every surviving piggybacked parity h
+    leaves in RS form, b(h) = original b(h) ^ XOR of XORSet(h)'s a-halves
+    (retrieveRS, xrs.go:305-320); everything else is unchanged."""
+    x = xrs_amd.XRS(D, P)
+    xs = x.xor_set
+    S, H = 16 * size, size // 2
+    t = _dev_random(n * S, cuda, 4321)
+    x.encode_batched(t.data_ptr(), size, size, S, n, stream())
+    torch.cuda.synchronize()
+    v = t.view(n, 16, size)
+    orig = v.clone()
+    for lost in ([0, 1], [0, 1, 2], [0, 1, 2, 3], [3, 9, 14], [5, 13]):
+        v.copy_(orig)
+        v[:, lost] = 0x5A
+        has = [i for i in range(16) if i not in lost]
+        x.reconst_batched(t.data_ptr(), size, size, S, n, has, lost, stream())
+        torch.cuda.synchronize()
+        exp = orig.clone()
+        for h in has:
+            if h > D and xs.get(h):
+                piggy = orig[:, xs[h][0], :H].clone()
+                for j in xs[h][1:]:
+                    piggy ^= orig[:, j, :H]
+                exp[:, h, H:] ^= piggy
+        assert torch.equal(v, exp), lost
+        del exp
+    del t, v, orig
+    torch.cuda.empty_cache()
+
+
 def test_update_linearity_full_size(cuda):
     """BASELINE config 4 (8 MiB vects): Update then Update back is the identity,
     and Update equals re-encode on sampled stripes."""

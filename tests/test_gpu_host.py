@@ -23,13 +23,11 @@ def pinned(nbytes):
 
 
 @pytest.mark.parametrize("size,n", [(4096, 5000), (1 << 20, 70), (1026, 333), (8 << 20, 9)])
-@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable", "pageable_dma"])
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
 def test_encode_host_vs_oracle(rng, monkeypatch, size, n, mode):
     """Pinned memory runs the kernels in place over PCIe (zero copy) unless
     XRS_HOST_ZC=0 selects the copy pipeline; pageable memory always copies."""
-    pin = not mode.startswith("pageable")
-    if mode == "pageable_dma":  # the DMA pipeline instead of pooled staging
-        monkeypatch.setenv("XRS_HOST_STAGE", "0")
+    pin = mode != "pageable"
     if mode == "pinned_dma":
         monkeypatch.setenv("XRS_HOST_ZC", "0")
     stripe = 16 * size
@@ -104,14 +102,12 @@ def test_host_zero_copy_inside_allocation(rng):
 
 
 @pytest.mark.parametrize("size,n", [(4096, 3000), (1026, 257), (1 << 20, 9)])
-@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable", "pageable_dma"])
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
 def test_reconst_host_vs_oracle(rng, monkeypatch, size, n, mode):
     """xrs_reconst_host on a host-resident batch: clean loss patterns (only
     survivors up, written halves back) and unclean ones (repeated index, need
     inside dpHas: whole stripes both ways), side effects included."""
-    pin = not mode.startswith("pageable")
-    if mode == "pageable_dma":  # the DMA pipeline instead of pooled staging
-        monkeypatch.setenv("XRS_HOST_STAGE", "0")
+    pin = mode != "pageable"
     if mode == "pinned_dma":
         monkeypatch.setenv("XRS_HOST_ZC", "0")
     stripe = 16 * size
@@ -142,14 +138,12 @@ def test_reconst_host_vs_oracle(rng, monkeypatch, size, n, mode):
 
 
 @pytest.mark.parametrize("size,n", [(4096, 2000), (1026, 100), (1 << 20, 6)])
-@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable", "pageable_dma"])
+@pytest.mark.parametrize("mode", ["pinned_zero_copy", "pinned_dma", "pageable"])
 def test_update_replace_host_vs_oracle(rng, monkeypatch, size, n, mode):
     """xrs_update_host / xrs_replace_host: old, new, data and parity in
     separate host buffers (pinned in place, pinned copy pipeline, pageable);
     parity equals the oracle's per-stripe Update / Replace."""
-    pin = not mode.startswith("pageable")
-    if mode == "pageable_dma":  # the DMA pipeline instead of pooled staging
-        monkeypatch.setenv("XRS_HOST_STAGE", "0")
+    pin = mode != "pageable"
     if mode == "pinned_dma":
         monkeypatch.setenv("XRS_HOST_ZC", "0")
     allocs = []

@@ -9,15 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
-#include <memory>
 #include <mutex>
-#include <thread>
 #include <vector>
 
 #include "gf256.h"
@@ -27,69 +22,6 @@
 using xrs::GF;
 using xrs::GfTab;
 using xrs::RowRef;
-
-namespace {
-
-// A fixed set of host threads that run `fn(i)` for i in [0, n) together with
-// the calling thread (the host-resident pipeline's gathers and scatters
-// between pageable caller memory and pinned staging).
-class CopyPool {
- public:
-  explicit CopyPool(int threads) {
-    for (int t = 0; t < threads; ++t) th_.emplace_back([this] { loop(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  void run(size_t n, const std::function<void(size_t)>& fn) {
-    if (n == 0) return;
-    std::unique_lock<std::mutex> lk(mu_);
-    fn_ = &fn;
-    n_ = n;
-    next_.store(0);
-    pending_ = th_.size();
-    ++gen_;
-    lk.unlock();
-    cv_.notify_all();
-    work();
-    lk.lock();
-    done_cv_.wait(lk, [this] { return pending_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  void work() {
-    for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
-  }
-  void loop() {
-    uint64_t seen = 0;
-    std::unique_lock<std::mutex> lk(mu_);
-    for (;;) {
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-      if (stop_) return;
-      seen = gen_;
-      lk.unlock();
-      work();
-      lk.lock();
-      if (--pending_ == 0) done_cv_.notify_all();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0, pending_ = 0;
-  std::atomic<size_t> next_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
-}  // namespace
 
 struct xrs_codec {
   int d = 0, p = 0;
@@ -120,12 +52,6 @@ struct xrs_codec {
   mutable uint8_t* slot[kPipe] = {nullptr, nullptr, nullptr};
   mutable size_t slot_cap = 0;
   mutable hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
-  // pageable batches: pinned, device-mapped staging slots filled and drained
-  // by a host thread pool; the kernels run on them in place over PCIe
-  mutable uint8_t* hslot[kPipe] = {nullptr, nullptr, nullptr};
-  mutable uint8_t* hslot_dev[kPipe] = {nullptr, nullptr, nullptr};
-  mutable size_t hslot_cap = 0;
-  mutable std::unique_ptr<CopyPool> pool;
 
   uint8_t g(int row, int col) const { return gen[static_cast<size_t>(row) * d + col]; }
 };
@@ -821,134 +747,13 @@ struct HostBatch {
   }
 };
 
-// Pinned, device-mapped staging slots and the copy pool (caller holds pipe_mu).
-int ensure_hpipe(const xrs_codec* x, size_t bytes) {
-  if (x->device < 0) return XRS_ERR_NO_DEVICE;
-  for (int i = 0; i < xrs_codec::kPipe; ++i)
-    if (!x->pstream[i] && hipStreamCreateWithFlags(&x->pstream[i], hipStreamNonBlocking) != hipSuccess)
-      return XRS_ERR_HIP;
-  if (bytes > x->hslot_cap) {
-    for (int i = 0; i < xrs_codec::kPipe; ++i) {
-      if (x->hslot[i]) (void)hipHostFree(x->hslot[i]);
-      x->hslot[i] = x->hslot_dev[i] = nullptr;
-    }
-    x->hslot_cap = 0;
-    for (int i = 0; i < xrs_codec::kPipe; ++i) {
-      void* dp = nullptr;
-      if (hipHostMalloc(&x->hslot[i], bytes, hipHostMallocMapped) != hipSuccess ||
-          hipHostGetDevicePointer(&dp, x->hslot[i], 0) != hipSuccess || !dp)
-        return XRS_ERR_HIP;
-      x->hslot_dev[i] = static_cast<uint8_t*>(dp);
-    }
-    x->hslot_cap = bytes;
-  }
-  if (!x->pool) {  // XRS_HOST_THREADS copy threads in all, the caller's included
-    const size_t t = std::min<size_t>(env_size("XRS_HOST_THREADS", 8), 64);
-    x->pool.reset(new CopyPool(t > 1 ? static_cast<int>(t - 1) : 0));
-  }
-  return XRS_OK;
-}
-
-// Pageable host batches (disk / NIC buffers the caller did not pin): chunk c
-// is gathered by the copy pool into a pinned, device-mapped staging slot, the
-// kernel runs on the slot in place over PCIe (no DMA), and the written pieces
-// are scattered back by the pool while the next chunk's kernel runs.  With
-// the gathers of chunk c+1 overlapping the kernel of chunk c, the pageable
-// rate approaches the pinned in-place one.  gather(s, st) / scatter(s, st)
-// copy stripe s of the batch into / out of its staged stripe st (dev_stripe
-// bytes); launch(slot, n, stream) runs the op on the compact staged layout.
-// XRS_HOST_STAGE=0 (or XRS_HOST_ZC=0) uses the DMA pipelines below (A/B).
-template <class Gather, class Scatter, class Launch>
-int run_staged(const xrs_codec* x, size_t n_stripes, size_t dev_stripe, Gather gather,
-               Scatter scatter, Launch launch) {
-  const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
-  std::lock_guard<std::mutex> lk(x->pipe_mu);
-  DeviceGuard g(x->device);
-  int e = ensure_hpipe(x, chunk * dev_stripe);
-  if (e) return e;
-  const size_t task = std::max<size_t>(1, (1u << 20) / dev_stripe);  // ~1 MiB of copies
-  auto copy = [&](size_t c0, size_t nc, int si, bool in) {
-    uint8_t* slot = x->hslot[si];
-    x->pool->run((nc + task - 1) / task, [&](size_t t) {
-      const size_t s1 = std::min(nc, (t + 1) * task);
-      for (size_t s = t * task; s < s1; ++s) {
-        if (in) gather(c0 + s, slot + s * dev_stripe);
-        else scatter(c0 + s, slot + s * dev_stripe);
-      }
-    });
-  };
-  size_t prev_c0 = 0, prev_nc = 0;
-  int prev_si = -1;
-  size_t i = 0;
-  for (size_t c0 = 0; c0 < n_stripes && !e; c0 += chunk, ++i) {
-    const int si = static_cast<int>(i % xrs_codec::kPipe);
-    const size_t nc = std::min(chunk, n_stripes - c0);
-    copy(c0, nc, si, true);  // overlaps the previous chunk's kernel
-    e = launch(x->hslot_dev[si], nc, x->pstream[si]);
-    if (prev_si >= 0) {
-      const int es = hip_err(hipStreamSynchronize(x->pstream[prev_si]));
-      if (!e) e = es;
-      if (!e) copy(prev_c0, prev_nc, prev_si, false);  // overlaps this chunk's kernel
-    }
-    prev_c0 = c0;
-    prev_nc = nc;
-    prev_si = si;
-  }
-  if (prev_si >= 0) {
-    const int es = hip_err(hipStreamSynchronize(x->pstream[prev_si]));
-    if (!e) e = es;
-    if (!e) copy(prev_c0, prev_nc, prev_si, false);
-  }
-  return e;
-}
-
-// run_staged for a batch in one host allocation: `in` / `out` are the
-// (shard, half) pieces moved per stripe (half: 0 = a, 1 = b, 2 = whole vect).
-template <class Launch>
-int run_pipeline_staged(const xrs_codec* x, const HostBatch& hb,
-                        const std::vector<std::pair<int, int>>& in,
-                        const std::vector<std::pair<int, int>>& out, Launch launch) {
-  const size_t S = hb.size, H = S / 2;
-  const size_t dev_stripe = static_cast<size_t>(x->d + x->p) * S;
-  struct Piece {
-    int shard;
-    size_t off, len;
-  };
-  auto pieces = [&](const std::vector<std::pair<int, int>>& v) {
-    std::vector<Piece> r;
-    for (auto& p : v) r.push_back({p.first, p.second == 1 ? H : 0, p.second == 2 ? S : H});
-    return r;
-  };
-  const std::vector<Piece> pin = pieces(in), pout = pieces(out);
-  return run_staged(
-      x, hb.n_stripes, dev_stripe,
-      [&](size_t s, uint8_t* st) {
-        for (const Piece& p : pin)
-          std::memcpy(st + static_cast<size_t>(p.shard) * S + p.off, hb.row(s, p.shard, p.off), p.len);
-      },
-      [&](size_t s, uint8_t* st) {
-        for (const Piece& p : pout)
-          std::memcpy(hb.row(s, p.shard, p.off), st + static_cast<size_t>(p.shard) * S + p.off, p.len);
-      },
-      launch);
-}
-
-bool host_stage_enabled() {
-  const char* v = std::getenv("XRS_HOST_STAGE");
-  const char* z = std::getenv("XRS_HOST_ZC");
-  return !(v && v[0] == '0') && !(z && z[0] == '0');
-}
-
 // Chunked H2D -> kernel -> D2H over kPipe streams.  `in` / `out` list the
 // (shard, half) pieces moved per stripe (half: 0 = a, 1 = b, 2 = whole vect);
 // `launch(slot_base, n, stream)` runs the op on the compact device layout.
-// Pageable batches take run_pipeline_staged unless XRS_HOST_STAGE=0 or
-// XRS_HOST_ZC=0.
 template <class Launch>
 int run_pipeline(const xrs_codec* x, const HostBatch& hb,
                  const std::vector<std::pair<int, int>>& in,
                  const std::vector<std::pair<int, int>>& out, Launch launch) {
-  if (host_stage_enabled()) return run_pipeline_staged(x, hb, in, out, launch);
   const int nshards = x->d + x->p;
   const size_t S = hb.size, H = S / 2;
   const size_t dev_stripe = static_cast<size_t>(nshards) * S;
@@ -1006,16 +811,6 @@ template <class Launch>
 int run_pipeline_rows(const xrs_codec* x, size_t n_stripes, size_t dev_stripe,
                       const std::vector<HostRows>& in, const std::vector<HostRows>& out,
                       Launch launch) {
-  if (host_stage_enabled())
-    return run_staged(
-        x, n_stripes, dev_stripe,
-        [&](size_t s, uint8_t* st) {
-          for (const HostRows& r : in) std::memcpy(st + r.dev_off, r.host + s * r.stride, r.len);
-        },
-        [&](size_t s, uint8_t* st) {
-          for (const HostRows& r : out) std::memcpy(r.host + s * r.stride, st + r.dev_off, r.len);
-        },
-        launch);
   const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
   std::lock_guard<std::mutex> lk(x->pipe_mu);
   DeviceGuard g(x->device);
@@ -1151,7 +946,6 @@ void xrs_free(xrs_codec* x) {
     for (int i = 0; i < xrs_codec::kPipe; ++i) {
       if (x->pstream[i]) (void)hipStreamDestroy(x->pstream[i]);
       if (x->slot[i]) (void)hipFree(x->slot[i]);
-      if (x->hslot[i]) (void)hipHostFree(x->hslot[i]);
     }
   }
   delete x;

@@ -162,9 +162,10 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); default: WORLD_SIZE, else 1")
-    # 200 steps = ~0.65 s of timed GPU work at N = 1 (long enough for the
-    # driver's GPU-busy sampling to see it; the whole run stays ~30 s)
-    ap.add_argument("--steps", type=int, default=200)
+    # 500 steps = ~1.6 s of timed GPU work at N = 1, so the driver's GPU-busy
+    # sampling can see it (1,000 steps read within 0.2% of 200:
+    # profiles/r02_steps_ab.jsonl); the whole run stays ~35 s
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--enc-stripes", type=int, default=65536)
     ap.add_argument("--rec-stripes", type=int, default=512)

@@ -149,6 +149,26 @@ def main():
                 emit(f"reconst_one_{d}+{p}", size, n, secs,
                      n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
                 del t
+    if "rows_bs" in cases:  # ReconstOne @ 4 KiB: 256- vs 1024-thread blocks, other codecs
+        for d, p in ((12, 3), (16, 4), (14, 4), (12, 4), (10, 4)):
+            xo = xrs_amd.XRS(d, p)
+            size = 4096
+            n = (4 << 30) // ((d + p) * size)
+            shard, stripe = xrs_amd.batch_strides(size, d + p)
+            t = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device=dev)
+            a_need, _ = xo.get_need_vects(0)
+            res = {}
+            for rnd in range(2):
+                for bs in ("256", "1024"):
+                    os.environ["XRS_ROWS_BLOCK"] = bs
+                    secs = timed(lambda i: xo.reconst_one_batched(t.data_ptr(), size, shard, stripe,
+                                                                  n, 0, s))
+                    res[bs] = min(res.get(bs, 1e9), secs)
+            os.environ.pop("XRS_ROWS_BLOCK", None)
+            for bs, secs in res.items():
+                emit(f"reconst_one_{d}+{p}_block_{bs}", size, n, secs,
+                     n * ((d - 1 + 2 + len(a_need)) * size // 2 + size), shard)
+            del t
     if "replace_ab" in cases:  # Replace(n): compile-time vs runtime source count
         for size, n in ((4096, 65536), (8 << 20, 32)):
             t, sh, st = batch(size, n, dev, 7)

@@ -1128,7 +1128,15 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   if (a.total == 0) return 0;
   // 1024-thread blocks for rows of >= 256 KiB (ReconstOne at 1 MiB vects:
   // +3-5% over 256, profiles/r01_blocksize.log); XRS_ROWS_BLOCK=256 for A/B.
-  const int bs = (VEC && p.len >= (256u << 10)) ? env_block("XRS_ROWS_BLOCK", 1024) : kBlock;
+  // Also 1024 for the compile-time shapes of 18-22 rows on rows of up to
+  // 4 KiB (ReconstOne 16+4 / 14+4 @ 4 KiB +3.5% / +1.9%; 12+3 even; 12+4, 16
+  // rows, -10%: profiles/r02_rows_bs.log).  XRS_ROWS_BLOCK=1024 forces it at
+  // any length (A/B), =256 turns both rules off.
+  constexpr bool kWide = NM != kDyn && NM + NX >= 18 && NM + NX <= 22;
+  const char* rbv = std::getenv("XRS_ROWS_BLOCK");
+  const bool force1024 = rbv && std::atoi(rbv) == 1024;
+  const bool big = p.len >= (256u << 10) || (kWide && p.len <= 4096) || force1024;
+  const int bs = (VEC && big) ? env_block("XRS_ROWS_BLOCK", 1024) : kBlock;
   const uint64_t blocks = (a.total + bs - 1) / bs;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kRows, VEC, p.len, blocks, bs);

@@ -85,3 +85,38 @@ def test_launch_local_propagates_a_failed_rank(tmp_path):
                             timeout=240)
     assert rc == 3
     assert not (tmp_path / "result.json").exists()
+
+
+def test_launch_local_sigterm_stops_the_ranks(tmp_path):
+    """SIGTERM to the launching parent stops every rank it started (a
+    driver's time limit must not leave ranks holding GPUs)."""
+    import signal
+    import time
+    rank = tmp_path / "rank.py"
+    rank.write_text("import os, sys, time\n"
+                    "d = sys.argv[1]\n"
+                    "open(os.path.join(d, 'pid' + os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                    "time.sleep(600)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text("import sys\n"
+                      f"sys.path.insert(0, {ROOT!r})\n"
+                      "from xrs_amd import dist as xdist\n"
+                      f"sys.exit(xdist.launch_local(2, [sys.executable, {str(rank)!r}, {str(tmp_path)!r}]))\n")
+    proc = subprocess.Popen([sys.executable, str(parent)])
+    deadline = time.monotonic() + 120
+    while len(list(tmp_path.glob("pid*"))) < 2 and time.monotonic() < deadline:
+        time.sleep(0.1)
+    time.sleep(0.2)
+    pids = [int(p.read_text()) for p in tmp_path.glob("pid*")]
+    assert len(pids) == 2
+    proc.send_signal(signal.SIGTERM)
+    assert proc.wait(timeout=60) != 0
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank {pid} still running")

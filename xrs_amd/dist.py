@@ -78,33 +78,48 @@ def launch_local(n: int, argv: Sequence[str], env=None, timeout: Optional[float]
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
                 LOCAL_WORLD_SIZE=str(n))
     procs: List[subprocess.Popen] = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen(list(argv), env=e))
-    t0 = time.monotonic()
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-        if rc != 0 or (timeout is not None and time.monotonic() - t0 > timeout):
-            if rc == 0:
-                rc = 124
-            for p in live:  # exactly the processes this call started
+
+    def stop(live):  # exactly the processes this call started
+        for p in live:
+            if p.poll() is None:
                 p.send_signal(signal.SIGTERM)
-            for p in live:
-                try:
-                    p.wait(timeout=30)
-                except subprocess.TimeoutExpired:
-                    p.kill()
-                    p.wait()
-            break
-        time.sleep(0.05)
+        for p in live:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    # A SIGTERM to this parent (a driver's time limit) must not orphan ranks
+    # that hold GPUs: turn it into an exception, so the finally below stops them.
+    def on_term(signum, frame):
+        raise SystemExit(128 + signum)
+
+    old = signal.signal(signal.SIGTERM, on_term)
+    rc = 0
+    live: List[subprocess.Popen] = []
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen(list(argv), env=e))
+        t0 = time.monotonic()
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+            if rc != 0 or (timeout is not None and time.monotonic() - t0 > timeout):
+                if rc == 0:
+                    rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        stop([p for p in procs if p.poll() is None])
+        signal.signal(signal.SIGTERM, old)
     return rc
 
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of one launch-time environment knob through the product
+launchers: VAR=XRS_PAIR_BLOCK VALS=256,128 CASE=encode SIZE=1048576 [CODEC=12,4]
+[ROUNDS=15] [STRIPES=n, default ~4 GiB of vects].  CASE is encode, reconst_one or reconst_2 (two lost data vects,
+staged path).  One JSON line per value: median GB/s of the bytes the launch
+moves (rounds alternate the values, so box drift hits both alike)."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import xrs_amd  # noqa: E402
+
+
+def main():
+    d, p = (int(v) for v in os.environ.get("CODEC", "12,4").split(","))
+    var = os.environ["VAR"]
+    vals = os.environ["VALS"].split(",")
+    case = os.environ.get("CASE", "encode")
+    size = int(os.environ.get("SIZE", str(1 << 20)))
+    rounds = int(os.environ.get("ROUNDS", "15"))
+    n = int(os.environ.get("STRIPES", "0")) or (4 << 30) // ((d + p) * size)
+    x = xrs_amd.XRS(d, p)
+    s = torch.cuda.current_stream().cuda_stream
+    shard, stripe = xrs_amd.batch_strides(size, d + p)
+    buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
+    b = buf.data_ptr()
+    if case == "encode":
+        moved = (d + p) * size * n
+        fn = lambda: x.encode_batched(b, size, shard, stripe, n, s)  # noqa: E731
+    elif case == "reconst_one":
+        a_need, _ = x.get_need_vects(3)
+        moved = ((d + 1 + len(a_need)) * size // 2 + size) * n
+        fn = lambda: x.reconst_one_batched(b, size, shard, stripe, n, 3, s)  # noqa: E731
+    elif case == "reconst_2":
+        moved = int(16.5 * size * n)
+        fn = lambda: x.reconst_batched(b, size, shard, stripe, n,  # noqa: E731
+                                       list(range(2, d + p)), [0, 1], s)
+    else:
+        raise SystemExit(f"unknown CASE {case}")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t = {v: [] for v in vals}
+    for _ in range(rounds):
+        for v in vals:
+            os.environ[var] = v
+            fn()
+            ev[0].record()
+            for _ in range(4):
+                fn()
+            ev[1].record()
+            ev[1].synchronize()
+            t[v].append(ev[0].elapsed_time(ev[1]) / 4)
+    for v in vals:
+        med = sorted(t[v])[rounds // 2]
+        print(json.dumps({"var": var, "val": v, "case": case, "size": size, "codec": f"{d}+{p}",
+                          "ms": round(med, 4), "gbs": round(moved / med / 1e6, 1)}))
+
+
+if __name__ == "__main__":
+    main()

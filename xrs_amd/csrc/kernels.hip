@@ -1016,12 +1016,15 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   a.total = a.chunks * p.n_stripes;
   if (a.total == 0) return 0;
   // 128-thread blocks for the 16-byte kernels on halves up to 4 KiB (Encode
-  // at 4 KiB +1-2.5% over 256; at 1 MiB -1.5..+0.9%, so 256 stays there:
-  // profiles/r01_blocksize.log).  XRS_PAIR_BLOCK=256 / 128 forces either.
+  // at 4 KiB +1-2.5% over 256: profiles/r01_blocksize.log) and for 12+
+  // sources at any size (interleaved A/B at 1 / 4 MiB: 12+4 +1.4 / -0.3%,
+  // 14+4 0 / +6%, 16+4 +8% @ 1 MiB, 20-28+4 -2..+7%); fewer sources keep 256
+  // (8+4, 10+2, 4+2: -1.4..-4.7% with 128): profiles/r02_pairblock_ab*.log.
+  // XRS_PAIR_BLOCK=256 / 128 forces either.
   const char* pb = std::getenv("XRS_PAIR_BLOCK");
   const int bs = !VEC ? kBlock
                       : (pb && *pb) ? env_block("XRS_PAIR_BLOCK", 128)
-                                    : (p.half <= 4096 ? 128 : kBlock);
+                                    : (p.half <= 4096 || n >= 12 ? 128 : kBlock);
   const uint64_t blocks = (a.total + bs - 1) / bs;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kPair, VEC, p.half, blocks, bs);

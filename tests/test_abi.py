@@ -151,8 +151,25 @@ def test_single_hip_runtime():
 def test_batch_strides_recommendation():
     """xrs_batch_strides (codec.cpp): shards back to back below 4 MiB, odd
     sizes back to back below 32 KiB, 16-rounded from there, a 4 KiB + 256 B
-    pad from 4 MiB up (profiles/r02_stride_probe.log, r01_order_ab.log)."""
+    pad from 4 MiB up (profiles/r02_stride_probe.log, r01_order_ab.log); the
+    stripe stride rounded up to a power of two when that costs at most 1/7
+    of the packed stripe (profiles/r02_layout_*.log)."""
     cases = {4096: 4096, 4100: 4100, 2: 2, 1026: 1026, 65536: 65536, 65538: 65552,
              1 << 20: 1 << 20, (1 << 20) + 2: (1 << 20) + 16, 8 << 20: (8 << 20) + 4352}
     for size, shard in cases.items():
         assert xrs_amd.batch_strides(size, 16) == (shard, 16 * shard), size
+    # 12+3: 15 x 4 KiB = 60 KiB -> 64 KiB (1/15 more); 10+4: 56 -> 64 KiB
+    # (exactly 1/7); 16+4: 80 KiB stays (128 KiB would cost 3/5 more)
+    assert xrs_amd.batch_strides(4096, 15) == (4096, 65536)
+    assert xrs_amd.batch_strides(4096, 14) == (4096, 65536)
+    assert xrs_amd.batch_strides(4096, 20) == (4096, 20 * 4096)
+    assert xrs_amd.batch_strides(4096, 9) == (4096, 9 * 4096)
+    assert xrs_amd.batch_strides(1 << 20, 15) == (1 << 20, 16 << 20)
+    assert xrs_amd.batch_strides(4 << 20, 15) == ((4 << 20) + 4352, 64 << 20)
+    assert xrs_amd.batch_strides(4100, 15) == (4100, 65536)  # odd sizes too (+3..6%)
+    assert xrs_amd.batch_strides(4100, 16) == (4100, 16 * 4100)
+    assert xrs_amd.batch_strides(4000, 16) == (4000, 65536)
+    for size in (1, 2, 100, 4096, 5000, 1 << 20, 3 << 20, 9 << 20):
+        for n in range(1, 40):
+            sh, st = xrs_amd.batch_strides(size, n)
+            assert sh >= size and n * sh <= st <= n * sh * 8 // 7, (size, n)

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of batch layouts (shard stride, stripe stride) for one
+launch: CODEC=12,3 SIZE=4096 CASE=reconst_one LAYOUTS=4096:61440,4096:65536
+[ROUNDS=15] [GIB=4].  A layout entry "shard:stripe" in bytes ("rec" = the
+library's recommendation).  One JSON line per layout: median GB/s of the
+bytes the launch moves."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import xrs_amd  # noqa: E402
+
+
+def main():
+    d, p = (int(v) for v in os.environ.get("CODEC", "12,3").split(","))
+    case = os.environ.get("CASE", "reconst_one")
+    size = int(os.environ.get("SIZE", "4096"))
+    rounds = int(os.environ.get("ROUNDS", "15"))
+    gib = float(os.environ.get("GIB", "4"))
+    n = int(gib * (1 << 30)) // ((d + p) * size)
+    x = xrs_amd.XRS(d, p)
+    s = torch.cuda.current_stream().cuda_stream
+    layouts = []
+    for e in os.environ.get("LAYOUTS", "rec").split(","):
+        if e == "rec":
+            layouts.append(("rec",) + tuple(xrs_amd.batch_strides(size, d + p)))
+        else:
+            sh, st = (int(v) for v in e.split(":"))
+            assert sh >= size and st >= (d + p) * sh
+            layouts.append((e, sh, st))
+    biggest = max(st for _, _, st in layouts)
+    buf = torch.randint(0, 256, (n * biggest,), dtype=torch.uint8, device="cuda")
+    b = buf.data_ptr()
+    a_need, _ = x.get_need_vects(3)
+    moved = {"encode": (d + p) * size * n,
+             "reconst_one": ((d + 1 + len(a_need)) * size // 2 + size) * n}[case]
+
+    def fn(sh, st):
+        if case == "encode":
+            x.encode_batched(b, size, sh, st, n, s)
+        else:
+            x.reconst_one_batched(b, size, sh, st, n, 3, s)
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t = {name: [] for name, _, _ in layouts}
+    for _ in range(rounds):
+        for name, sh, st in layouts:
+            fn(sh, st)
+            ev[0].record()
+            for _ in range(4):
+                fn(sh, st)
+            ev[1].record()
+            ev[1].synchronize()
+            t[name].append(ev[0].elapsed_time(ev[1]) / 4)
+    for name, sh, st in layouts:
+        med = sorted(t[name])[rounds // 2]
+        print(json.dumps({"layout": name, "shard_stride": sh, "stripe_stride": st, "case": case,
+                          "size": size, "codec": f"{d}+{p}", "stripes": n, "ms": round(med, 4),
+                          "gbs": round(moved / med / 1e6, 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,9 @@
 """Interleaved A/B of batch layouts (shard stride, stripe stride) for one
 launch: CODEC=12,3 SIZE=4096 CASE=reconst_one LAYOUTS=4096:61440,4096:65536
 [ROUNDS=15] [GIB=4].  A layout entry "shard:stripe" in bytes ("rec" = the
-library's recommendation).  One JSON line per layout: median GB/s of the
+library's recommendation; "sm" or "sm:PAD" = shard-major, each shard's
+rows back to back over the stripes: stripe stride = size, shard stride =
+n*size + PAD).  One JSON line per layout: median GB/s of the
 bytes the launch moves."""
 import json
 import os
@@ -28,22 +30,31 @@ def main():
     for e in os.environ.get("LAYOUTS", "rec").split(","):
         if e == "rec":
             layouts.append(("rec",) + tuple(xrs_amd.batch_strides(size, d + p)))
+        elif e.startswith("sm"):
+            pad = int(e[3:] or 0) if ":" in e else 0
+            layouts.append((e, n * size + pad, size))
         else:
             sh, st = (int(v) for v in e.split(":"))
             assert sh >= size and st >= (d + p) * sh
             layouts.append((e, sh, st))
-    biggest = max(st for _, _, st in layouts)
-    buf = torch.randint(0, 256, (n * biggest,), dtype=torch.uint8, device="cuda")
+    extent = max((n - 1) * st + (d + p - 1) * sh + size for _, sh, st in layouts)
+    buf = torch.randint(0, 256, (extent,), dtype=torch.uint8, device="cuda")
     b = buf.data_ptr()
     a_need, _ = x.get_need_vects(3)
+    # reconst_L: L lost data vects (staged kernel); bytes it moves at 12+4,
+    # side effects included (tools/order_sweep.py): 16.5 / 17.5 S at 2 / 4
     moved = {"encode": (d + p) * size * n,
-             "reconst_one": ((d + 1 + len(a_need)) * size // 2 + size) * n}[case]
+             "reconst_one": ((d + 1 + len(a_need)) * size // 2 + size) * n,
+             "reconst_2": int(16.5 * size * n), "reconst_4": int(17.5 * size * n)}[case]
 
     def fn(sh, st):
         if case == "encode":
             x.encode_batched(b, size, sh, st, n, s)
-        else:
+        elif case == "reconst_one":
             x.reconst_one_batched(b, size, sh, st, n, 3, s)
+        else:
+            lost = int(case[-1])
+            x.reconst_batched(b, size, sh, st, n, list(range(lost, d + p)), list(range(lost)), s)
 
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t = {name: [] for name, _, _ in layouts}

@@ -39,3 +39,21 @@ if [ -n "$ODD" ]; then
     OUT=r02_layout_odd run 12,3 $c 12304:184560,12304:196608 12304
   done
 fi
+if [ -n "$SM" ]; then
+  for c in reconst_one encode; do
+    OUT=r02_layout_sm run 12,4 $c rec,sm,sm:4352 4096
+    OUT=r02_layout_sm run 12,4 $c rec,sm,sm:4352 4100
+    OUT=r02_layout_sm run 12,4 $c rec,sm,sm:4352 1048578
+    OUT=r02_layout_sm run 12,4 $c rec,sm,sm:4352 1048576
+    OUT=r02_layout_sm run 12,3 $c rec,sm,sm:4352 4096
+    OUT=r02_layout_sm run 16,4 $c rec,sm,sm:4352 4096
+  done
+fi
+if [ -n "$STAGED" ]; then
+  for c in reconst_2 reconst_4; do
+    OUT=r02_layout_staged run 12,4 $c rec,1052672:16842752,1048832:16781312,1114112:17825792,1048576:20971520,1048576:33554432 1048576
+    OUT=r02_layout_staged run 12,4 $c rec,4352:69632,4096:98304,4096:131072 4096
+    OUT=r02_layout_staged run 12,4 $c rec,sm 1048576
+    OUT=r02_layout_staged run 12,4 $c rec,65792:1052672 65536
+  done
+fi

@@ -92,9 +92,11 @@ int xrs_replace(const xrs_codec *codec, uint8_t *const *data, const int *rows, i
 
 /* ---- batched, device-resident, async (the performance path) ----------- */
 /* Recommended device layout for a batch of stripes of n_shards vects of
- * `size` bytes: shard stride (size rounded up to 16, plus a 4 KiB + 256 B pad
- * from 4 MiB up) and stripe stride.  Any layout works; this one streams
- * fastest on MI355X. */
+ * `size` bytes: shard stride (size itself below 32 KiB, else size rounded
+ * up to 16; plus a 4 KiB + 256 B pad from 4 MiB up) and stripe
+ * stride (n_shards shard strides, rounded up to a power of two when that
+ * costs at most 1/7 more).  Any layout works; this one streams fastest on
+ * MI355X. */
 int xrs_batch_strides(size_t size, int n_shards, size_t *shard_stride, size_t *stripe_stride);
 /* Encode n_stripes stripes in place.  One fused pass: RS + piggyback. */
 int xrs_encode_batched(const xrs_codec *codec, uint8_t *base, size_t size,

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B of one launch-time environment knob through the product
 launchers: VAR=XRS_PAIR_BLOCK VALS=256,128 CASE=encode SIZE=1048576 [CODEC=12,4]
-[ROUNDS=15] [STRIPES=n, default ~4 GiB of vects].  CASE is encode, reconst_one or reconst_2 (two lost data vects,
-staged path).  One JSON line per value: median GB/s of the bytes the launch
+[ROUNDS=15] [STRIPES=n, default ~4 GiB of vects].  CASE is encode, reconst_one or reconst_2 / _3 / _4 (lost data
+vects, staged path).  One JSON line per value: median GB/s of the bytes the launch
 moves (rounds alternate the values, so box drift hits both alike)."""
 import json
 import os
@@ -35,17 +35,21 @@ def main():
         a_need, _ = x.get_need_vects(3)
         moved = ((d + 1 + len(a_need)) * size // 2 + size) * n
         fn = lambda: x.reconst_one_batched(b, size, shard, stripe, n, 3, s)  # noqa: E731
-    elif case == "reconst_2":
-        moved = int(16.5 * size * n)
+    elif case in ("reconst_2", "reconst_3", "reconst_4"):
+        lost = int(case[-1])  # bytes moved at 12+4, side effects included
+        moved = int({2: 16.5, 3: 17.0, 4: 17.5}[lost] * size * n)
         fn = lambda: x.reconst_batched(b, size, shard, stripe, n,  # noqa: E731
-                                       list(range(2, d + p)), [0, 1], s)
+                                       list(range(lost, d + p)), list(range(lost)), s)
     else:
         raise SystemExit(f"unknown CASE {case}")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t = {v: [] for v in vals}
     for _ in range(rounds):
         for v in vals:
-            os.environ[var] = v
+            if v:
+                os.environ[var] = v
+            else:  # an empty value = the library's default (variable unset)
+                os.environ.pop(var, None)
             fn()
             ev[0].record()
             for _ in range(4):

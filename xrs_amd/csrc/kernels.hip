@@ -816,8 +816,8 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks, int
     case Shape::kStaged:
       if (len <= 2048) o.k = static_cast<uint32_t>(blocks / 8);
       else if (len < (256u << 10)) o.k = 32;
-      else if (len < (1u << 20)) o.k = 128;
-      break;  // half >= 1 MiB: plain order
+      else o.k = 128;  // (plain order above 1 MiB halves: 2-11% slower at
+      break;           // 2, 8, 16 MiB vects, profiles/r02_staged_bigorder.log)
     case Shape::kRows:
       if (bs == 1024 && len >= (256u << 10)) {  // 16 KiB blocks: K = half / 4 KiB, <= 256
         o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 12));

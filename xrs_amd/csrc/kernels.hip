@@ -819,8 +819,10 @@ BlockOrder block_order(Shape shape, bool vec, uint64_t len, uint64_t blocks, int
       else o.k = 128;  // (plain order above 1 MiB halves: 2-11% slower at
       break;           // 2, 8, 16 MiB vects, profiles/r02_staged_bigorder.log)
     case Shape::kRows:
-      if (bs == 1024 && len >= (256u << 10)) {  // 16 KiB blocks: K = half / 4 KiB, <= 256
-        o.k = static_cast<uint32_t>(std::min<uint64_t>(256, len >> 12));
+      if (bs == 1024 && len >= (256u << 10)) {  // 16 KiB blocks: K = half / 4 KiB,
+        // 64 from 1 MiB halves (12+4 ReconstOne at 4 / 8 / 16 MiB vects +2 /
+        // +5 / +4% over 256: profiles/r02_bigorder.log, r02_enc_k0.log)
+        o.k = len >= (1u << 20) ? 64 : static_cast<uint32_t>(len >> 12);
         break;
       }
       if (len <= 4096) o.k = static_cast<uint32_t>(blocks / 8);
@@ -1028,6 +1030,12 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + bs - 1) / bs;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kPair, VEC, p.half, blocks, bs);
+  // The 12+4 Encode from 1 MiB vects up streams 2-5% faster in the plain
+  // block order (1, 1.5, 2, 4, 8 MiB; 768 KiB even, 512 KiB -1.3%); other
+  // codecs at 1 MiB lose 1-3% with it (profiles/r02_enc_k0*.log).
+  if (P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) &&
+      !std::getenv("XRS_BLOCK_ORDER"))
+    a.order.k = 0;
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC) {
     if (bs == 128) {

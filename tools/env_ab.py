@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B of one launch-time environment knob through the product
 launchers: VAR=XRS_PAIR_BLOCK VALS=256,128 CASE=encode SIZE=1048576 [CODEC=12,4]
-[ROUNDS=15] [STRIPES=n, default ~4 GiB of vects].  CASE is encode, reconst_one or reconst_2 / _3 / _4 (lost data
-vects, staged path).  One JSON line per value: median GB/s of the bytes the launch
+[ROUNDS=15] [STRIPES=n, default ~4 GiB of vects].  CASE is encode, reconst_one, reconst_2 / _3 / _4 (lost data
+vects, staged path), update or replace_K.  One JSON line per value: median GB/s of the bytes the launch
 moves (rounds alternate the values, so box drift hits both alike)."""
 import json
 import os
@@ -40,6 +40,16 @@ def main():
         moved = int({2: 16.5, 3: 17.0, 4: 17.5}[lost] * size * n)
         fn = lambda: x.reconst_batched(b, size, shard, stripe, n,  # noqa: E731
                                        list(range(lost, d + p)), list(range(lost)), s)
+    elif case == "update":  # one data row (3) of every stripe, new bytes back to back
+        new = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device="cuda")
+        moved = (2 * p + 2) * size * n
+        fn = lambda: x.update_batched(b + 3 * shard, stripe, new.data_ptr(), size,  # noqa: E731
+                                      size, 3, b + d * shard, shard, stripe, n, s)
+    elif case.startswith("replace_"):  # Replace(k): data rows 0..k-1
+        k = int(case.split("_")[1])
+        moved = (k + 2 * p) * size * n
+        fn = lambda: x.replace_batched(b, shard, stripe, list(range(k)), size,  # noqa: E731
+                                       b + d * shard, shard, stripe, n, s)
     else:
         raise SystemExit(f"unknown CASE {case}")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

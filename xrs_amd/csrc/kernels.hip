@@ -1033,9 +1033,14 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   // The 12+4 Encode from 1 MiB vects up streams 2-5% faster in the plain
   // block order (1, 1.5, 2, 4, 8 MiB; 768 KiB even, 512 KiB -1.3%); other
   // codecs at 1 MiB lose 1-3% with it (profiles/r02_enc_k0*.log).
-  if (P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) &&
-      !std::getenv("XRS_BLOCK_ORDER"))
+  // Update / Replace (accumulating) on halves up to 4 KiB: each XCD a
+  // contiguous eighth of the grid, as the rows kernel at 4 KiB (Replace(1, 2,
+  // 4, 8) @ 4 KiB +4-10%, @ 8 KiB +3-7%; Update +2%:
+  // profiles/r02_updrep_order*.log).
+  const bool forced = std::getenv("XRS_BLOCK_ORDER") != nullptr;
+  if (P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) && !forced)
     a.order.k = 0;
+  if (ACC && VEC && p.half <= 4096 && !forced) a.order.k = static_cast<uint32_t>(blocks / 8);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC) {
     if (bs == 128) {

@@ -33,13 +33,16 @@ def main():
         elif e.startswith("sm"):
             pad = int(e[3:] or 0) if ":" in e else 0
             layouts.append((e, n * size + pad, size))
-        else:
-            sh, st = (int(v) for v in e.split(":"))
+        else:  # "shard:stripe" or "shard:stripe@offset" (batch base + offset bytes)
+            lay, _, o = e.partition("@")
+            sh, st = (int(v) for v in lay.split(":"))
             assert sh >= size and st >= (d + p) * sh
             layouts.append((e, sh, st))
-    extent = max((n - 1) * st + (d + p - 1) * sh + size for _, sh, st in layouts)
+    offs = {name: int(name.partition("@")[2] or 0) for name, _, _ in layouts}
+    extent = max((n - 1) * st + (d + p - 1) * sh + size + offs[nm] for nm, sh, st in layouts)
     buf = torch.randint(0, 256, (extent,), dtype=torch.uint8, device="cuda")
-    b = buf.data_ptr()
+    b0 = buf.data_ptr()
+    assert b0 % 4096 == 0
     a_need, _ = x.get_need_vects(3)
     # reconst_L: L lost data vects (staged kernel); bytes it moves at 12+4,
     # side effects included (tools/order_sweep.py): 16.5 / 17.5 S at 2 / 4
@@ -47,7 +50,7 @@ def main():
              "reconst_one": ((d + 1 + len(a_need)) * size // 2 + size) * n,
              "reconst_2": int(16.5 * size * n), "reconst_4": int(17.5 * size * n)}[case]
 
-    def fn(sh, st):
+    def fn(sh, st, b):
         if case == "encode":
             x.encode_batched(b, size, sh, st, n, s)
         elif case == "reconst_one":
@@ -60,10 +63,10 @@ def main():
     t = {name: [] for name, _, _ in layouts}
     for _ in range(rounds):
         for name, sh, st in layouts:
-            fn(sh, st)
+            fn(sh, st, b0 + offs[name])
             ev[0].record()
             for _ in range(4):
-                fn(sh, st)
+                fn(sh, st, b0 + offs[name])
             ev[1].record()
             ev[1].synchronize()
             t[name].append(ev[0].elapsed_time(ev[1]) / 4)

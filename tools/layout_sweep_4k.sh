@@ -57,3 +57,16 @@ if [ -n "$STAGED" ]; then
     OUT=r02_layout_staged run 12,4 $c rec,65792:1052672 65536
   done
 fi
+if [ -n "$DELTA" ]; then
+  for c in reconst_one encode; do
+    OUT=r02_layout_delta run 12,4 $c rec,4096:65552,4096:65600,4096:65792,4096:66560,4096:69632,4096:73728,4096:98304,4096:131072 4096
+    OUT=r02_layout_delta run 12,4 $c 4100:65600,4100:65792,4100:66560,4100:69632,4100:81920,4100:98304,4100:131072 4100
+  done
+fi
+if [ -n "$ALIGN" ]; then
+  for c in reconst_one encode; do
+    OUT=r02_layout_align run 12,4 $c 4096:65536,4096:65536@16,4096:65536@64,4096:65536@128,4096:65536@256,4096:65536@1024,4096:65536@2048 4096
+    OUT=r02_layout_align run 12,4 $c 4100:65600,8192:131072,8192:131072@2046,4100:65600@2046 4100
+    OUT=r02_layout_align run 12,4 $c 1048576:16777216,1048576:16777216@16,1048576:16777216@256,1048576:16777216@2048 1048576
+  done
+fi

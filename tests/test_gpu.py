@@ -624,3 +624,54 @@ def test_replace_batched_every_n_vs_oracle(cuda, rng, monkeypatch, mode, size, n
             pv = [ref[st, q] for q in range(P)]
             o.replace([data[st, i].copy() for i in range(nrep)], rows, pv)
         assert np.array_equal(tp.cpu().numpy(), ref), (nrep, rows)
+
+
+@pytest.mark.parametrize("d,p,size", [(12, 3, 4096), (10, 4, 4096), (13, 2, 4100), (12, 3, 1 << 16),
+                                      (12, 4, 4096)])
+def test_recommended_layout_vs_oracle(cuda, rng, d, p, size):
+    """The layout xrs_batch_strides recommends (a power-of-two stripe stride
+    with a gap after the last shard when that costs <= 1/7, codec.cpp):
+    Encode, every ReconstOne and a 2-loss Reconst against the oracle, with
+    the gap bytes untouched."""
+    shard, stripe = xrs_amd.batch_strides(size, d + p)
+    n = 24
+    buf = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+
+    def rows(b, s):
+        return [b[s * stripe + i * shard:][:size] for i in range(d + p)]
+
+    ref = buf.copy()
+    for s in range(n):
+        v = [r.copy() for r in rows(ref, s)]
+        o.encode(v)
+        for i in range(d + p):
+            ref[s * stripe + i * shard:][:size] = v[i]
+    t = to_dev(buf, cuda)
+    x.encode_batched(t.data_ptr(), size, shard, stripe, n, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), ref)  # gaps included
+    for k in range(d):
+        t = to_dev(ref, cuda)
+        for s in range(n):
+            t[s * stripe + k * shard:s * stripe + k * shard + size] = 0x5A
+        x.reconst_one_batched(t.data_ptr(), size, shard, stripe, n, k, stream())
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), ref), k
+    lost = [0, d - 1]
+    has = [i for i in range(d + p) if i not in lost]
+    exp = ref.copy()
+    for s in range(n):
+        v = [r.copy() for r in rows(exp, s)]
+        for i in lost:
+            v[i][:] = 0
+        o.reconst(v, has, lost)
+        for i in range(d + p):
+            exp[s * stripe + i * shard:][:size] = v[i]
+    t = to_dev(ref, cuda)
+    for s in range(n):
+        for i in lost:
+            t[s * stripe + i * shard:s * stripe + i * shard + size] = 0
+    x.reconst_batched(t.data_ptr(), size, shard, stripe, n, has, lost, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), exp)

@@ -257,7 +257,7 @@ def headline(R: Rank, args):
          n_enc * 8 * ENC_S,
          lambda i: x.reconst_one_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
                                          i % D, s)),
-        ("encode_1m", "pair_kernel<4,12,false,true,128>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
+        ("encode_1m", "pair_kernel<4,12,false,true,128,true>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
          lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, s)),
         ("reconst_one_1m", "rows_kernel<2,12,4,false,true,1024>", n_rec * 9 * REC_S,
          n_rec * 8 * REC_S,

@@ -207,6 +207,51 @@ def main():
             for (bs, lost), secs in sorted(res.items()):
                 emit(f"reconst_{lost}_block_{bs}", size, n, secs, n * (D + lost) * size, sh)
             del t
+    if "multi_bs_order" in cases:  # staged Reconst: block size x order x early/late
+        sizes = ((1 << 20, 256), (256 << 10, 1024), (4096, 65536))
+        for size, n in sizes:
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(2):
+                for bs in ("128", "256"):
+                    os.environ["XRS_STAGED_BLOCK"] = bs
+                    for early in ("0", "1"):
+                        os.environ["XRS_STAGED_EARLY"] = early
+                        for order in ("", "0", "16", "32", "64", "128", "256"):
+                            if order:
+                                os.environ["XRS_BLOCK_ORDER"] = order
+                            else:
+                                os.environ.pop("XRS_BLOCK_ORDER", None)
+                            for lost in (2, 4):
+                                need, has = list(range(lost)), list(range(lost, D + P))
+                                secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st,
+                                                                         n, has, need, s), ramp=0.05)
+                                k = (bs, early, order or "def", lost)
+                                res[k] = min(res.get(k, 1e9), secs)
+            for v in ("XRS_STAGED_BLOCK", "XRS_STAGED_EARLY", "XRS_BLOCK_ORDER"):
+                os.environ.pop(v, None)
+            for (bs, early, order, lost), secs in sorted(res.items()):
+                emit(f"reconst_{lost}_bs{bs}_early{early}_order{order}", size, n, secs,
+                     n * (D + lost) * size, sh)
+            del t
+    if "multi_npre" in cases:  # staged Reconst: b-row loads issued with the a-rows
+        for size, n in ((4096, 65536), (64 << 10, 4096), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(3):  # interleaved rounds, best of each
+                for npre in ("0", "4", "6", "8", "all"):
+                    os.environ["XRS_STAGED_NPRE"] = "-1" if npre == "all" else npre
+                    for lost in (2, 3, 4):
+                        need, has = list(range(lost)), list(range(lost, D + P))
+                        secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n,
+                                                                 has, need, s))
+                        res[(npre, lost)] = min(res.get((npre, lost), 1e9), secs)
+            os.environ.pop("XRS_STAGED_NPRE", None)
+            for (npre, lost), secs in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+                emit(f"reconst_{lost}_npre_{npre}", size, n, secs, n * (D + lost) * size, sh)
+            del t
     if "multi_order" in cases:  # staged Reconst (compile-time kernel) in every block order
         sizes = ((4096, 65536), (1 << 20, 256))
         if os.environ.get("MULTI_SIZES"):  # e.g. MULTI_SIZES=1048576

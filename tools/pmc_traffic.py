@@ -24,7 +24,7 @@ from collections import defaultdict
 KERNELS = {
     "encode_4k": ("pair_kernel<4, 12, false, true, 128>", 65536 * 128),
     "reconst_one_4k": ("rows_kernel<2, 12, 4, false, true, 256>", 65536 * 128),
-    "encode_1m": ("pair_kernel<4, 12, false, true, 128>", 512 * 32768),
+    "encode_1m": ("pair_kernel<4, 12, false, true, 128, true>", 512 * 32768),
     "reconst_one_1m": ("rows_kernel<2, 12, 4, false, true, 1024>", 512 * 32768),
 }
 ALGO_BYTES = {"encode_4k": 65536 * 16 * 4096, "reconst_one_4k": 65536 * 9 * 4096,

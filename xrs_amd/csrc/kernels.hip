@@ -212,10 +212,15 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
   }
 }
 
-template <int P, int C, bool ACC, bool VEC, int BS = kBlock>
+// PLAIN: the plain block order known at compile time (no logical_block map);
+// used by the 12+4 Encode from 512 KiB halves, which streams fastest in the
+// plain order (launch_pair_t).  It also gives that launch, the bench's
+// dominant one, its own name in rocprofv3 --stats (the 4 KiB Encode runs the
+// same <4, 12, false, true, 128> shape in the XCD order).
+template <int P, int C, bool ACC, bool VEC, int BS = kBlock, bool PLAIN = false>
 __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
+  const uint64_t gid = (PLAIN ? uint64_t(blockIdx.x) : logical_block(a.order)) * BS + threadIdx.x;
   if (gid >= a.total) return;
   const uint64_t stripe = gid / a.chunks;
   uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
@@ -659,8 +664,11 @@ __device__ __forceinline__ void stw(const uint32_t* v, uint64_t addr) {
   }
 }
 
-template <int ND, int NB, int NL, int NN, int BS, bool EARLY = false>
+// NPRE: b-rows whose loads are issued with the a-rows (0: after stage 1,
+// "late"; NB: every row's load in flight at once, "early").
+template <int ND, int NB, int NL, int NN, int BS, int NPRE = 0>
 __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, true> a) {
+  static_assert(NPRE >= 0 && NPRE <= NB, "NPRE");
   constexpr int W = 4;
   const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
   if (gid >= a.total) return;
@@ -671,10 +679,8 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int m = 0; m < ND; ++m) ldw<W>(xa[m], row_addr(a.asrc[m], stripe, off));
-  if constexpr (EARLY) {  // every row's load in flight at once (one round trip)
 #pragma unroll
-    for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
-  }
+  for (int m = 0; m < NPRE; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
   __builtin_amdgcn_s_setprio(0);
   // Stage 1: lost a-halves (xrs.go:247-262).
 #pragma unroll
@@ -701,10 +707,10 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
 #pragma unroll
   for (int q = 0; q < NL; ++q) stw<W>(al[q], row_addr(a.adst[q], stripe, off));
 
-  if constexpr (!EARLY) {
+  if constexpr (NPRE < NB) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+    for (int m = NPRE; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
     __builtin_amdgcn_s_setprio(0);
   }
 #pragma unroll
@@ -841,18 +847,22 @@ int env_block(const char* var, int def) {
   return (v == 256 || v == def) ? v : def;
 }
 
-template <int NL, int NN, int BS, bool EARLY>
+// NPRE < 0: every b-row early (NPRE = NB).
+template <int NL, int NN, int BS, int NPRE>
 int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + BS - 1) / BS;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, true, p.half, blocks, BS);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == 12)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, NPRE < 0 ? 12 : NPRE>), g, dim3(BS), 0,
+                       stream, a);
   else if (p.nb == 13)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, NPRE < 0 ? 13 : NPRE>), g, dim3(BS), 0,
+                       stream, a);
   else
-    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, EARLY>), g, dim3(BS), 0, stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, NPRE < 0 ? 14 : NPRE>), g, dim3(BS), 0,
+                       stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -927,8 +937,13 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // XRS_STAGED_EARLY=0 / =1 forces either (A/B, tests).
       const char* ev = std::getenv("XRS_STAGED_EARLY");
       const bool early = (ev && *ev) ? ev[0] == '1' : p.half < (256u << 10);
-      if (early) return launch_staged_ct_bs<NL, NN, kBlock, true>(a, p, stream);
-      return launch_staged_ct_bs<NL, NN, kBlock, false>(a, p, stream);
+      // XRS_STAGED_BLOCK=128: 128-thread blocks (A/B)
+      if (env_block("XRS_STAGED_BLOCK", 128) == 128 && std::getenv("XRS_STAGED_BLOCK")) {
+        if (early) return launch_staged_ct_bs<NL, NN, 128, -1>(a, p, stream);
+        return launch_staged_ct_bs<NL, NN, 128, 0>(a, p, stream);
+      }
+      if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
+      return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
     }
   }
   if (late)
@@ -1038,10 +1053,17 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   // 4, 8) @ 4 KiB +4-10%, @ 8 KiB +3-7%; Update +2%:
   // profiles/r02_updrep_order*.log).
   const bool forced = std::getenv("XRS_BLOCK_ORDER") != nullptr;
-  if (P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) && !forced)
-    a.order.k = 0;
+  const bool plain12 = P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) && !forced;
+  if (plain12) a.order.k = 0;
   if (ACC && VEC && p.half <= 4096 && !forced) a.order.k = static_cast<uint32_t>(blocks / 8);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  if constexpr (VEC && P == 4 && C == 12 && !ACC) {
+    if (plain12) {
+      hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC, 128, true>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(128), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if constexpr (VEC) {
     if (bs == 128) {
       hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC, 128>), dim3(static_cast<unsigned>(blocks)),

@@ -250,9 +250,11 @@ def oracle_encode_batch(o, host):
     return h
 
 
-@pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 65536])
+# 1 MiB and 1 MiB + 2: the 12+4 Encode from 512 KiB halves runs the
+# plain-order kernel specialization (pair_kernel<4, 12, false, true, 128, true>)
+@pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 65536, 1 << 20, (1 << 20) + 2])
 def test_encode_batched_vs_oracle(cuda, rng, size):
-    n = max(1, (8 << 20) // (16 * size))
+    n = max(3, (8 << 20) // (16 * size))
     host = batch(rng, n, size)
     t = to_dev(host, cuda)
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)

@@ -215,7 +215,7 @@ def main():
             res = {}
             for rnd in range(2):
                 for bs in ("128", "256"):
-                    os.environ["XRS_STAGED_BLOCK"] = bs
+                    os.environ["XRS_STAGED_BLOCK"] = bs  # (knob removed after this sweep)
                     for early in ("0", "1"):
                         os.environ["XRS_STAGED_EARLY"] = early
                         for order in ("", "0", "16", "32", "64", "128", "256"):

@@ -937,11 +937,10 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // XRS_STAGED_EARLY=0 / =1 forces either (A/B, tests).
       const char* ev = std::getenv("XRS_STAGED_EARLY");
       const bool early = (ev && *ev) ? ev[0] == '1' : p.half < (256u << 10);
-      // XRS_STAGED_BLOCK=128: 128-thread blocks (A/B)
-      if (env_block("XRS_STAGED_BLOCK", 128) == 128 && std::getenv("XRS_STAGED_BLOCK")) {
-        if (early) return launch_staged_ct_bs<NL, NN, 128, -1>(a, p, stream);
-        return launch_staged_ct_bs<NL, NN, 128, 0>(a, p, stream);
-      }
+      // (b-row loads split between the phases, 4 / 6 / 8 with the a-rows:
+      // within 1% of the better end; 128-thread blocks x every block order:
+      // the defaults within 1% of the best at 4 KiB, 256 KiB and 1 MiB:
+      // profiles/r02_staged_npre.log, r02_staged_bs_order.log)
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
     }

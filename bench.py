@@ -251,7 +251,7 @@ def headline(R: Rank, args):
     # The four timed launches of a step, in order: (key, kernel, algorithmic
     # bytes per launch, read bytes per launch, launcher).
     launches = [
-        ("encode_4k", "pair_kernel<4,12,false,true,128>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
+        ("encode_4k", "pair_kernel<4,12,false,true,128,false>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
          lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s)),
         ("reconst_one_4k", "rows_kernel<2,12,4,false,true,256>", n_enc * 9 * ENC_S,
          n_enc * 8 * ENC_S,

@@ -235,6 +235,33 @@ def main():
                 emit(f"reconst_{lost}_bs{bs}_early{early}_order{order}", size, n, secs,
                      n * (D + lost) * size, sh)
             del t
+    if "multi_big_bs" in cases:  # staged Reconst, late kernel: 512/1024-thread blocks x order
+        for size, n in ((1 << 20, 256), (256 << 10, 1024)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(2):
+                for bs in ("", "512", "1024"):
+                    if bs:
+                        os.environ["XRS_STAGED_BLOCK"] = bs
+                    else:
+                        os.environ.pop("XRS_STAGED_BLOCK", None)
+                    for order in ("", "8", "16", "32", "64", "128"):
+                        if order:
+                            os.environ["XRS_BLOCK_ORDER"] = order
+                        else:
+                            os.environ.pop("XRS_BLOCK_ORDER", None)
+                        for lost in (2, 4):
+                            need, has = list(range(lost)), list(range(lost, D + P))
+                            secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n,
+                                                                     has, need, s), ramp=0.05)
+                            k = (bs or "def", order or "def", lost)
+                            res[k] = min(res.get(k, 1e9), secs)
+            for v in ("XRS_STAGED_BLOCK", "XRS_BLOCK_ORDER"):
+                os.environ.pop(v, None)
+            for (bs, order, lost), secs in sorted(res.items()):
+                emit(f"reconst_{lost}_bs{bs}_order{order}", size, n, secs, n * (D + lost) * size, sh)
+            del t
     if "multi_npre" in cases:  # staged Reconst: b-row loads issued with the a-rows
         for size, n in ((4096, 65536), (64 << 10, 4096), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

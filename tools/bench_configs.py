@@ -262,6 +262,30 @@ def main():
             for (bs, order, lost), secs in sorted(res.items()):
                 emit(f"reconst_{lost}_bs{bs}_order{order}", size, n, secs, n * (D + lost) * size, sh)
             del t
+    if "multi_big_confirm" in cases:  # staged Reconst: default vs 1024-thread blocks, K 32 / 64
+        for size in (512 << 10, 1 << 20, 2 << 20, 8 << 20):
+            n = (4 << 30) // (16 * size)
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(3):
+                for bs, order in (("", ""), ("1024", "32"), ("1024", "64"), ("1024", "")):
+                    for v, val in (("XRS_STAGED_BLOCK", bs), ("XRS_BLOCK_ORDER", order)):
+                        if val:
+                            os.environ[v] = val
+                        else:
+                            os.environ.pop(v, None)
+                    for lost in (2, 3, 4):
+                        need, has = list(range(lost)), list(range(lost, D + P))
+                        secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n,
+                                                                 has, need, s), ramp=0.05)
+                        k = (bs or "def", order or "def", lost)
+                        res[k] = min(res.get(k, 1e9), secs)
+            for v in ("XRS_STAGED_BLOCK", "XRS_BLOCK_ORDER"):
+                os.environ.pop(v, None)
+            for (bs, order, lost), secs in sorted(res.items()):
+                emit(f"reconst_{lost}_bs{bs}_order{order}", size, n, secs, n * (D + lost) * size, sh)
+            del t
     if "multi_npre" in cases:  # staged Reconst: b-row loads issued with the a-rows
         for size, n in ((4096, 65536), (64 << 10, 4096), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

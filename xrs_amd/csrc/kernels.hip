@@ -940,11 +940,9 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // (b-row loads split between the phases, 4 / 6 / 8 with the a-rows:
       // within 1% of the better end; 128-thread blocks x every block order:
       // the defaults within 1% of the best at 4 KiB, 256 KiB and 1 MiB:
-      // profiles/r02_staged_npre.log, r02_staged_bs_order.log)
-      if (const char* bv = std::getenv("XRS_STAGED_BLOCK")) {  // A/B: late kernel, big blocks
-        if (std::atoi(bv) == 512) return launch_staged_ct_bs<NL, NN, 512, 0>(a, p, stream);
-        if (std::atoi(bv) == 1024) return launch_staged_ct_bs<NL, NN, 1024, 0>(a, p, stream);
-      }
+      // profiles/r02_staged_npre.log, r02_staged_bs_order.log; the late
+      // kernel in 512- and 1024-thread blocks, K = 8..128, from 512 KiB to
+      // 8 MiB vects: -3..+2.3%, within noise: r02_staged_big_{bs,confirm}.log)
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
     }

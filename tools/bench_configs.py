@@ -286,6 +286,23 @@ def main():
             for (bs, order, lost), secs in sorted(res.items()):
                 emit(f"reconst_{lost}_bs{bs}_order{order}", size, n, secs, n * (D + lost) * size, sh)
             del t
+    if "multi_il" in cases:  # staged Reconst, every load first: a/b of a survivor back to back
+        for size, n in ((4096, 65536), (16384, 16384), (64 << 10, 4096), (256 << 10, 1024)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            res = {}
+            for rnd in range(4):
+                for il in ("0", "1"):
+                    os.environ["XRS_STAGED_IL"] = il
+                    for lost in (2, 3, 4):
+                        need, has = list(range(lost)), list(range(lost, D + P))
+                        secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n,
+                                                                 has, need, s), ramp=0.05)
+                        res[(il, lost)] = min(res.get((il, lost), 1e9), secs)
+            os.environ.pop("XRS_STAGED_IL", None)
+            for (il, lost), secs in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+                emit(f"reconst_{lost}_il{il}", size, n, secs, n * (D + lost) * size, sh)
+            del t
     if "multi_npre" in cases:  # staged Reconst: b-row loads issued with the a-rows
         for size, n in ((4096, 65536), (64 << 10, 4096), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

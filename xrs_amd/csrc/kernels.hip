@@ -855,14 +855,14 @@ int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStre
   a.order = block_order(Shape::kStaged, true, p.half, blocks, BS);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == 12)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, NPRE < 0 ? 12 : NPRE>), g, dim3(BS), 0,
-                       stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, NPRE < 0 ? 12 : NPRE>), g, dim3(BS),
+                       0, stream, a);
   else if (p.nb == 13)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, NPRE < 0 ? 13 : NPRE>), g, dim3(BS), 0,
-                       stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, NPRE < 0 ? 13 : NPRE>), g, dim3(BS),
+                       0, stream, a);
   else
-    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, NPRE < 0 ? 14 : NPRE>), g, dim3(BS), 0,
-                       stream, a);
+    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, NPRE < 0 ? 14 : NPRE>), g, dim3(BS),
+                       0, stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -942,7 +942,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // the defaults within 1% of the best at 4 KiB, 256 KiB and 1 MiB:
       // profiles/r02_staged_npre.log, r02_staged_bs_order.log; the late
       // kernel in 512- and 1024-thread blocks, K = 8..128, from 512 KiB to
-      // 8 MiB vects: -3..+2.3%, within noise: r02_staged_big_{bs,confirm}.log)
+      // 8 MiB vects: -3..+2.3%, within noise: r02_staged_big_{bs,confirm}.log;
+      // each survivor's a- and b-half loads back to back: +-1%, r02_staged_il.log)
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
     }

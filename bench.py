@@ -162,16 +162,16 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); default: WORLD_SIZE, else 1")
-    # 500 steps = ~1.6 s of timed GPU work at N = 1, so the driver's GPU-busy
-    # sampling can see it (1,000 steps read within 0.2% of 200:
-    # profiles/r02_steps_ab.jsonl); the whole run stays ~35 s
-    ap.add_argument("--steps", type=int, default=500)
+    # 1,500 steps = ~4.9 s of timed GPU work at N = 1, so the driver's
+    # GPU-busy sampling can see it (1,000 steps read within 0.2% of 200:
+    # profiles/r02_steps_ab.jsonl); the whole run stays under a minute
+    ap.add_argument("--steps", type=int, default=1500)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--enc-stripes", type=int, default=65536)
     ap.add_argument("--rec-stripes", type=int, default=512)
     ap.add_argument("--config5-stripes", type=int, default=8192,
                     help="1 MiB stripes per rank for the config5 key (0: skip)")
-    ap.add_argument("--config5-steps", type=int, default=5)
+    ap.add_argument("--config5-steps", type=int, default=20)  # ~3.5 s of GPU work
     ap.add_argument("--host-mib", type=int, default=1024,
                     help="MiB per host-resident batch for the host_e2e key (0: skip)")
     ap.add_argument("--xgmi-stripes", type=int, default=64,

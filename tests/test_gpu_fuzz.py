@@ -6,7 +6,10 @@ offset 0..15 so both the 16-byte and the byte-granular kernels run) and one
 operation (Encode, ReconstOne, Reconst with random losses and needs, Update,
 Replace).  The GPU buffer after the call must equal the oracle applied stripe
 by stripe to a host copy, byte for byte, including every byte outside the
-shards (nothing else may be written).  Seeded; bounded to a few seconds."""
+shards (nothing else may be written).  Seeded; bounded to a few seconds.
+XRS_FUZZ_SEEDS=N runs N seeds per test instead of 10 (long campaigns)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -18,12 +21,19 @@ pytestmark = pytest.mark.gpu
 
 CODECS = [(12, 4), (10, 4), (6, 3), (4, 2), (5, 5), (20, 4), (1, 2), (30, 6), (3, 9), (16, 8)]
 OPS = ["encode", "reconst_one", "reconst", "update", "replace"]
+SEEDS = int(os.environ.get("XRS_FUZZ_SEEDS", "10"))
+
+
+BIG = os.environ.get("XRS_FUZZ_BIG") == "1"  # long campaigns: also 128 KiB-1 MiB vects
 
 
 def draw_case(rng):
     d, p = CODECS[int(rng.integers(0, len(CODECS)))]
     size = int(rng.choice([2, 34, 1024, 1026, 4096, 4112, 6000, 40960]))
     n = int(rng.integers(1, 40))
+    if BIG and rng.integers(0, 4) == 0:
+        size = int(rng.choice([131072, 131074, 262160, 1048576, 1048578]))
+        n = int(rng.integers(1, 4))
     shard = size + int(rng.choice([0, 0, 2, 16, 256]))
     stripe = (d + p) * shard + int(rng.choice([0, 0, 6, 64]))
     base = int(rng.choice([0, 0, 0, 1, 8]))
@@ -35,7 +45,7 @@ def vects_of(buf, base, s, shard, stripe, size, count, first=0):
     return [buf[o + (first + i) * shard: o + (first + i) * shard + size] for i in range(count)]
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(SEEDS))
 def test_batched_fuzz_vs_oracle(seed):
     rng = np.random.Generator(np.random.PCG64(9000 + seed))
     dev = torch.device("cuda:0")
@@ -102,7 +112,7 @@ def test_batched_fuzz_vs_oracle(seed):
             raise AssertionError(f"{tag}: {len(bad)} bytes differ, first at {bad[0]}")
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(max(1, SEEDS * 2 // 5)))
 def test_sync_fuzz_vs_oracle(seed):
     """The per-stripe sync API (host vects: separate, oddly aligned numpy
     slices, sizes spanning the zero-copy / pinned / direct staging modes) on

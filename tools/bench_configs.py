@@ -303,6 +303,20 @@ def main():
             for (il, lost), secs in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
                 emit(f"reconst_{lost}_il{il}", size, n, secs, n * (D + lost) * size, sh)
             del t
+    if "multi_mixed" in cases:  # Reconst with lost parity in the loss pattern (xrs.go:236-301)
+        # bytes: the reference's accounting generalised, (d + lost) * S per
+        # stripe (d survivors read, the lost vects written)
+        pats = [([13], [13]), ([12], [12]), ([0, 13], [0, 13]), ([0, 12], [0, 12]),
+                ([0, 1, 13], [0, 1, 13]), ([0, 1, 12, 13], [0, 1, 12, 13]), ([0, 13], [0])]
+        for size, n in ((4096, 65536), (1 << 20, 256)):
+            t, sh, st = batch(size, n, dev, 5)
+            x.encode_batched(t.data_ptr(), size, sh, st, n, s)
+            for lost, need in pats:
+                has = [i for i in range(D + P) if i not in lost]
+                secs = timed(lambda i: x.reconst_batched(t.data_ptr(), size, sh, st, n, has, need, s))
+                tag = "lost" + "-".join(map(str, lost)) + "_need" + "-".join(map(str, need))
+                emit(f"reconst_{tag}", size, n, secs, n * (D + len(lost)) * size, sh)
+            del t
     if "multi_npre" in cases:  # staged Reconst: b-row loads issued with the a-rows
         for size, n in ((4096, 65536), (64 << 10, 4096), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)

@@ -307,7 +307,7 @@ def main():
         # bytes: the reference's accounting generalised, (d + lost) * S per
         # stripe (d survivors read, the lost vects written)
         pats = [([13], [13]), ([12], [12]), ([0, 13], [0, 13]), ([0, 12], [0, 12]),
-                ([0, 1, 13], [0, 1, 13]), ([0, 1, 12, 13], [0, 1, 12, 13]), ([0, 13], [0])]
+                ([0, 1, 13], [0, 1, 13]), ([0, 1, 12, 13], [0, 1, 12, 13])]
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)

@@ -195,7 +195,7 @@ def test_reconst_every_loss_pattern(rng, reconst_mode, order):
                 assert np.array_equal(a[i], b[i]), (lost, order, i)
 
 
-@pytest.mark.parametrize("ct", ["1", "0", "early", "late"])
+@pytest.mark.parametrize("ct", ["1", "0", "early", "late", "ws128", "ws256", "ws512", "ws128o5"])
 @pytest.mark.parametrize("size,n", [(4096, 600), (1 << 20, 4), (4112, 520)])
 def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     """General Reconst of batches large enough for the bandwidth kernels
@@ -203,8 +203,11 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     runtime-count one), side effects included, every stripe vs the oracle."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("XRS_STAGED_CT", "0" if ct == "0" else "1")
+    monkeypatch.delenv("XRS_STAGED_WS", raising=False)
     if ct in ("early", "late"):  # both phase layouts of the compile-time kernel
         monkeypatch.setenv("XRS_STAGED_EARLY", "1" if ct == "early" else "0")
+    if ct.startswith("ws"):  # the wave-specialised kernel, T chunks per block
+        monkeypatch.setenv("XRS_STAGED_WS", ct[2:])
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
     host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
     o.encode_batch(host, size, n)

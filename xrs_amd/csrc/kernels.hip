@@ -731,6 +731,101 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
   for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
 }
 
+// Wave-specialised variant of staged_ct_kernel: a block of 2*T lanes works on
+// T chunks.  Lanes [0, T) ("a-lanes") load the ND a-rows, rebuild the lost
+// a-halves and form the retrieveRS / re-piggyback XOR terms; lanes [T, 2T)
+// ("b-lanes") issue their NB b-row loads at the same time.  The XOR terms go
+// through LDS (one barrier), then the b-lanes finish stages 2-4.  Every wave
+// pays one memory round trip, as Encode does, and holds only its own rows
+// (the one-wave-does-both kernels pay two round trips, or hold every row at
+// once at 144-161 VGPRs).
+template <int ND, int NB, int NL, int NN, int T, int OCC = 1>
+__global__ __launch_bounds__(2 * T) __attribute__((amdgpu_waves_per_eu(OCC)))
+void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
+  constexpr int W = 4;
+  __shared__ uint4 xfer[kStOut + NN][T];  // rx[0..nr), then ob[0..NN)
+  const bool blane = threadIdx.x >= T;
+  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * T + t;
+  const bool valid = gid < a.total;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  uint32_t xb[NB][W];
+  if (!blane) {
+    if (valid) {
+      uint32_t xa[ND][W], al[NL][W];
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < ND; ++m) ldw<W>(xa[m], row_addr(a.asrc[m], stripe, off));
+      __builtin_amdgcn_s_setprio(0);
+      // Stage 1: lost a-halves (xrs.go:247-262).
+#pragma unroll
+      for (int q = 0; q < NL; ++q)
+#pragma unroll
+        for (int w = 0; w < W; ++w) al[q][w] = 0u;
+#pragma unroll
+      for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+      if constexpr (ND & 1) rows_mac1<NL, W>(al, a.at[ND - 1], xa[ND - 1]);
+      // XOR terms of stage 2 (retrieveRS, xrs.go:305-320) and stage 4
+      // (re-piggyback, :281-297) for the b-lanes.
+#pragma unroll
+      for (int r = 0; r < kStOut; ++r)
+        if (r < a.nr) {
+          uint32_t v[W] = {0u, 0u, 0u, 0u};
+          abar_ct<ND, NL, W>(v, a.rmask[r], xa, al);
+          xfer[r][t] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+      for (int u = 0; u < NN; ++u) {
+        uint32_t v[W] = {0u, 0u, 0u, 0u};
+        if (a.nmask[u]) abar_ct<ND, NL, W>(v, a.nmask[u], xa, al);
+        xfer[kStOut + u][t] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+#pragma unroll
+      for (int q = 0; q < NL; ++q) stw<W>(al[q], row_addr(a.adst[q], stripe, off));
+    }
+  } else if (valid) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // LDS only: the b-lanes' row loads stay in flight across the barrier.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  if (!blane || !valid) return;
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int r = 0; r < kStOut; ++r)
+      if (r < a.nr && a.rb[r] == m) {
+        const uint4 v = xfer[r][t];
+        xb[m][0] ^= v.x;
+        xb[m][1] ^= v.y;
+        xb[m][2] ^= v.z;
+        xb[m][3] ^= v.w;
+      }
+  uint32_t ob[NN][W];
+#pragma unroll
+  for (int u = 0; u < NN; ++u) {
+    const uint4 v = xfer[kStOut + u][t];
+    ob[u][0] = v.x;
+    ob[u][1] = v.y;
+    ob[u][2] = v.z;
+    ob[u][3] = v.w;
+  }
+  // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
+#pragma unroll
+  for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+  if constexpr (ND & 1) rows_mac1<NN, W>(ob, a.bt[ND - 1], xb[ND - 1]);
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+    if ((a.bstore >> m) & 1u) stw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+#pragma unroll
+  for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
+}
+
 // ============================================================ update_rows kernel
 // Update with a per-stripe data row (xrs_plan.h UpdRowsPlan).  The row's
 // coefficient tables are read from the kernel arguments with a per-lane index
@@ -847,6 +942,26 @@ int env_block(const char* var, int def) {
   return (v == 256 || v == def) ? v : def;
 }
 
+// Wave-specialised staged kernel: T chunks per block of 2*T lanes.
+template <int NL, int NN, int T, int OCC = 1>
+int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+  const uint64_t blocks = (a.total + T - 1) / T;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
+  if (const char* e = std::getenv("XRS_WS_ORDER")) {  // A/B knob
+    a.order.k = std::strcmp(e, "full") == 0 ? static_cast<uint32_t>(blocks / 8)
+                                            : static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+  }
+  const dim3 g(static_cast<unsigned>(blocks));
+  if (p.nb == 12)
+    hipLaunchKernelGGL((staged_ws_kernel<12, 12, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+  else if (p.nb == 13)
+    hipLaunchKernelGGL((staged_ws_kernel<12, 13, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+  else
+    hipLaunchKernelGGL((staged_ws_kernel<12, 14, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 // NPRE < 0: every b-row early (NPRE = NB).
 template <int NL, int NN, int BS, int NPRE>
 int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
@@ -944,6 +1059,14 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // kernel in 512- and 1024-thread blocks, K = 8..128, from 512 KiB to
       // 8 MiB vects: -3..+2.3%, within noise: r02_staged_big_{bs,confirm}.log;
       // each survivor's a- and b-half loads back to back: +-1%, r02_staged_il.log)
+      // XRS_STAGED_WS=128 / 256: the wave-specialised kernel, T chunks per block.
+      if (const char* wv = std::getenv("XRS_STAGED_WS")) {
+        if (std::strcmp(wv, "128") == 0) return launch_staged_ws<NL, NN, 128>(a, p, stream);
+        if (std::strcmp(wv, "256") == 0) return launch_staged_ws<NL, NN, 256>(a, p, stream);
+        if (std::strcmp(wv, "64") == 0) return launch_staged_ws<NL, NN, 64>(a, p, stream);
+        if (std::strcmp(wv, "512") == 0) return launch_staged_ws<NL, NN, 512>(a, p, stream);
+        if (std::strcmp(wv, "128o5") == 0) return launch_staged_ws<NL, NN, 128, 5>(a, p, stream);
+      }
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
     }
@@ -1054,9 +1177,15 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   // contiguous eighth of the grid, as the rows kernel at 4 KiB (Replace(1, 2,
   // 4, 8) @ 4 KiB +4-10%, @ 8 KiB +3-7%; Update +2%:
   // profiles/r02_updrep_order*.log).
+  // A batch of 48 GiB or more of 12+4 stripes streams best in K = 128
+  // instead (8,192 x 1 MiB = 128 GiB: plain 6.04 TB/s, K = 128 6.13; 64 GiB:
+  // 6.13 / 6.15; 32 GiB: plain +2.3%: profiles/r02_c5_order.log).
   const bool forced = std::getenv("XRS_BLOCK_ORDER") != nullptr;
-  const bool plain12 = P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) && !forced;
+  const bool enc12 = P == 4 && C == 12 && !ACC && bs == 128 && p.half >= (512u << 10) && !forced;
+  const bool huge = p.n_stripes * 32 * p.half >= (48ull << 30);
+  const bool plain12 = enc12 && !huge;
   if (plain12) a.order.k = 0;
+  if (enc12 && huge) a.order.k = 128;
   if (ACC && VEC && p.half <= 4096 && !forced) a.order.k = static_cast<uint32_t>(blocks / 8);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC && P == 4 && C == 12 && !ACC) {

@@ -204,8 +204,9 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("XRS_STAGED_CT", "0" if ct == "0" else "1")
     monkeypatch.delenv("XRS_STAGED_WS", raising=False)
-    if ct in ("early", "late"):  # both phase layouts of the compile-time kernel
+    if ct in ("early", "late"):  # both phase layouts of the one-wave compile-time kernel
         monkeypatch.setenv("XRS_STAGED_EARLY", "1" if ct == "early" else "0")
+        monkeypatch.setenv("XRS_STAGED_WS", "0")
     if ct.startswith("ws"):  # the wave-specialised kernel, T chunks per block
         monkeypatch.setenv("XRS_STAGED_WS", ct[2:])
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)

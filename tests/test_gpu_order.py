@@ -46,14 +46,16 @@ def test_encode_and_reconst_one_every_order(rng, monkeypatch, order, size, n):
     assert np.array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("variant", ["late", "0"])
+@pytest.mark.parametrize("variant", ["late", "late_one_wave", "0"])
 @pytest.mark.parametrize("order", ["0", "32", "full"])
 @pytest.mark.parametrize("size,n", [(4096, 513), (1 << 20, 9)])
 def test_staged_reconst_every_order(rng, monkeypatch, variant, order, size, n):
-    """Three lost data vects through every staged kernel variant, side effects
-    included."""
+    """Three lost data vects through every staged kernel variant (late: the
+    wave-specialised kernel; late_one_wave: the compile-time one-wave kernel;
+    0: all loads first), side effects included."""
     monkeypatch.setenv("XRS_BLOCK_ORDER", order)
-    monkeypatch.setenv("XRS_STAGED_LATE", variant)
+    monkeypatch.setenv("XRS_STAGED_LATE", "0" if variant == "0" else "1")
+    monkeypatch.setenv("XRS_STAGED_WS", "0" if variant == "late_one_wave" else "")
     host, t = batch(rng, size, n)
     o = OracleXRS(D, P)
     o.encode_batch(host, size, n)

@@ -115,9 +115,11 @@ def main():
         for size, n in ((4096, 65536), (1 << 20, 256)):
             t, sh, st = batch(size, n, dev, 5)
             x.encode_batched(t.data_ptr(), size, sh, st, n, s)
-            for mode in ("ct", "ct_early", "late", "early", "steps"):
-                # read per call by the library
+            for mode in ("ct", "ct_onewave", "ct_early", "late", "early", "steps"):
+                # read per call by the library ("ct": the default, the
+                # wave-specialised kernel at 2-3 lost; "ct_onewave": without it)
                 os.environ["XRS_RECONST"] = mode
+                os.environ["XRS_STAGED_WS"] = "" if mode == "ct" else "0"
                 os.environ["XRS_STAGED_LATE"] = "0" if mode == "early" else "1"
                 os.environ["XRS_STAGED_CT"] = "1" if mode.startswith("ct") else "0"
                 os.environ["XRS_STAGED_EARLY"] = "1" if mode == "ct_early" else "0"
@@ -133,6 +135,7 @@ def main():
             os.environ.pop("XRS_STAGED_LATE", None)
             os.environ.pop("XRS_STAGED_CT", None)
             os.environ.pop("XRS_STAGED_EARLY", None)
+            os.environ.pop("XRS_STAGED_WS", None)
             del t
     if "others" in cases:  # other (d, p): runtime-count kernels
         for d, p in ((10, 4), (6, 3), (8, 4), (4, 2), (16, 4), (20, 4), (12, 3)):

@@ -1059,8 +1059,17 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // kernel in 512- and 1024-thread blocks, K = 8..128, from 512 KiB to
       // 8 MiB vects: -3..+2.3%, within noise: r02_staged_big_{bs,confirm}.log;
       // each survivor's a- and b-half loads back to back: +-1%, r02_staged_il.log)
-      // XRS_STAGED_WS=128 / 256: the wave-specialised kernel, T chunks per block.
-      if (const char* wv = std::getenv("XRS_STAGED_WS")) {
+      // 2-3 lost: the wave-specialised kernel, 256 chunks per 512-lane block
+      // (bytes moved, interleaved medians vs the kernels above: 2 lost @ 4 KiB
+      // / 64 KiB / 256 KiB / 1 MiB +5.5 / +0.5 / +2.1 / 0%, 3 lost +4.0 /
+      // +0.5 / +1.4 / +6.5%; 4 lost -1..-7%, so it keeps the one-wave kernel;
+      // 64-, 128- and 512-chunk blocks and a 5-wave VGPR cap: no better
+      // overall; profiles/r02_staged_ws.log).  XRS_STAGED_WS=0 / 64 / 128 /
+      // 256 / 512 / 128o5 forces it off or a block size (A/B, tests).
+      const char* wv = std::getenv("XRS_STAGED_WS");
+      if (!wv || !*wv) {
+        if (NL <= 3) return launch_staged_ws<NL, NN, 256>(a, p, stream);
+      } else {
         if (std::strcmp(wv, "128") == 0) return launch_staged_ws<NL, NN, 128>(a, p, stream);
         if (std::strcmp(wv, "256") == 0) return launch_staged_ws<NL, NN, 256>(a, p, stream);
         if (std::strcmp(wv, "64") == 0) return launch_staged_ws<NL, NN, 64>(a, p, stream);

@@ -195,15 +195,20 @@ def test_reconst_every_loss_pattern(rng, reconst_mode, order):
                 assert np.array_equal(a[i], b[i]), (lost, order, i)
 
 
-@pytest.mark.parametrize("ct", ["1", "0", "early", "late", "ws128", "ws256", "ws512", "ws128o5"])
+@pytest.mark.parametrize("ct", ["1", "0", "0_onewave", "early", "late", "ws128", "ws256", "ws512",
+                                "ws128o5"])
 @pytest.mark.parametrize("size,n", [(4096, 600), (1 << 20, 4), (4112, 520)])
 def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     """General Reconst of batches large enough for the bandwidth kernels
     (compile-time staged kernel for lost data vects, XRS_STAGED_CT=0 the
     runtime-count one), side effects included, every stripe vs the oracle."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("XRS_STAGED_CT", "0" if ct == "0" else "1")
+    monkeypatch.setenv("XRS_STAGED_CT", "0" if ct.startswith("0") else "1")
     monkeypatch.delenv("XRS_STAGED_WS", raising=False)
+    if ct == "0_onewave":  # the runtime-count one-wave late kernel
+        monkeypatch.setenv("XRS_STAGED_WS", "0")
+    if ct == "0":  # the runtime-count wave-specialised kernel
+        monkeypatch.setenv("XRS_STAGED_WS", "rt")
     if ct in ("early", "late"):  # both phase layouts of the one-wave compile-time kernel
         monkeypatch.setenv("XRS_STAGED_EARLY", "1" if ct == "early" else "0")
         monkeypatch.setenv("XRS_STAGED_WS", "0")
@@ -224,6 +229,39 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
         got = t.cpu().numpy()
         for st in range(n):
             w = [h[st, i].copy() for i in range(D + P)]
+            o.reconst(w, has, need)
+            assert np.array_equal(got[st], np.stack(w)), (lost, need, st)
+
+
+@pytest.mark.parametrize("ws", ["", "0", "rt"])
+@pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4)])
+@pytest.mark.parametrize("size,n", [(4096, 520), (1 << 20, 4)])
+def test_reconst_batched_runtime_shapes_vs_oracle(rng, monkeypatch, ws, d, p, size, n):
+    """General Reconst on full grids through the runtime-count staged kernels
+    (default: wave-specialised for one lost parity; XRS_STAGED_WS=rt
+    wave-specialised for every pattern, =0 the one-wave late kernel):
+    other codecs and loss patterns with parity in them, side effects included,
+    every stripe vs the oracle."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("XRS_STAGED_WS", ws)
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    s = torch.cuda.current_stream().cuda_stream
+    last = d + p - 1
+    pats = [([0, 1], [0, 1]), ([d + 1], [d + 1]), ([d], [d]), ([0, d + 1], [0, d + 1]),
+            ([1, 2, last], [1, 2, last]), ([0, 1, d, d + 1][:p], [0, 1, d, d + 1][:p]),
+            ([3, d + 1], [3])]
+    for lost, need in pats:
+        h = host.copy()
+        h[:, lost] = 0xC3
+        has = [i for i in range(d + p) if i not in lost]
+        t = torch.from_numpy(h).cuda()
+        x.reconst_batched(t.data_ptr(), size, size, (d + p) * size, n, has, need, s)
+        torch.cuda.synchronize()
+        got = t.cpu().numpy()
+        for st in range(n):
+            w = [h[st, i].copy() for i in range(d + p)]
             o.reconst(w, has, need)
             assert np.array_equal(got[st], np.stack(w)), (lost, need, st)
 

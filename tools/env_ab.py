@@ -36,10 +36,16 @@ def main():
         moved = ((d + 1 + len(a_need)) * size // 2 + size) * n
         fn = lambda: x.reconst_one_batched(b, size, shard, stripe, n, 3, s)  # noqa: E731
     elif case in ("reconst_2", "reconst_3", "reconst_4"):
-        lost = int(case[-1])  # bytes moved at 12+4, side effects included
-        moved = int({2: 16.5, 3: 17.0, 4: 17.5}[lost] * size * n)
+        lost = int(case[-1])  # bytes moved at 12+4, side effects included (else accounted)
+        moved = int({2: 16.5, 3: 17.0, 4: 17.5}[lost] * size * n) if (d, p) == (12, 4) \
+            else (d + lost) * size * n
         fn = lambda: x.reconst_batched(b, size, shard, stripe, n,  # noqa: E731
                                        list(range(lost, d + p)), list(range(lost)), s)
+    elif case.startswith("mixed_"):  # mixed_0-13: those vects lost and needed, (d + lost) * S
+        lost = [int(v) for v in case.split("_")[1].split("-")]
+        has = [i for i in range(d + p) if i not in lost]
+        moved = (d + len(lost)) * size * n
+        fn = lambda: x.reconst_batched(b, size, shard, stripe, n, has, lost, s)  # noqa: E731
     elif case == "update":  # one data row (3) of every stripe, new bytes back to back
         new = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device="cuda")
         moved = (2 * p + 2) * size * n

@@ -826,6 +826,110 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
 }
 
+// Runtime-count form of staged_ws_kernel (any codec with d <= 16, lost parity
+// in the pattern, nl != nn): a-lanes load na a-rows, b-lanes nb b-rows, each
+// role's guarded loads issued together (each role waits once, so the
+// vmcnt(0) the waitcnt pass puts after guarded loads costs no extra round
+// trip).  Same conditions as staged_late_kernel: every retrieveRS row is
+// written back and there are at most kStOut of them.
+template <int NL, int NN, int T>
+__global__ __launch_bounds__(2 * T) void staged_ws_rt_kernel(const StagedArgs<NL, NN, true> a) {
+  constexpr int W = 4;
+  constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
+  __shared__ uint4 xfer[kStOut + N1][T];
+  const bool blane = threadIdx.x >= T;
+  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * T + t;
+  const bool valid = gid < a.total;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  const int nd = a.nd;
+  uint32_t xb[kStSrc][W];
+  if (!blane) {
+    if (valid) {
+      uint32_t xa[kStSrc][W], al[L1][W];
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < kStSrc; ++m)
+        if (m < a.na) ldw<W>(xa[m], row_addr(a.asrc[m], stripe, off));
+      __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+      for (int q = 0; q < L1; ++q)
+#pragma unroll
+        for (int w = 0; w < W; ++w) al[q][w] = 0u;
+      if constexpr (NL > 0) {
+        // Stage 1: lost a-halves (xrs.go:247-262).
+#pragma unroll
+        for (int m = 0; m < kStSrc; m += 2) {
+          if (m + 1 < nd) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
+          else if (m < nd) rows_mac1<NL, W>(al, a.at[m], xa[m]);
+        }
+      }
+      // XOR terms of stages 2 and 4 for the b-lanes.
+#pragma unroll
+      for (int r = 0; r < kStOut; ++r)
+        if (r < a.nr) {
+          uint32_t v[W] = {0u, 0u, 0u, 0u};
+          abar_xor<NL, W>(v, a.rmask[r], xa, al);
+          xfer[r][t] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+      for (int u = 0; u < NN; ++u) {
+        uint32_t v[W] = {0u, 0u, 0u, 0u};
+        if (a.nmask[u]) abar_xor<NL, W>(v, a.nmask[u], xa, al);
+        xfer[kStOut + u][t] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+      if constexpr (NL > 0) {
+#pragma unroll
+        for (int q = 0; q < NL; ++q)
+          if (q < a.nl) stw<W>(al[q], row_addr(a.adst[q], stripe, off));
+      }
+    }
+  } else if (valid) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < kStSrc; ++m)
+      if (m < a.nb) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  if (!blane || !valid) return;
+#pragma unroll
+  for (int m = 0; m < kStSrc; ++m)
+#pragma unroll
+    for (int r = 0; r < kStOut; ++r)
+      if (r < a.nr && a.rb[r] == m) {
+        const uint4 v = xfer[r][t];
+        xb[m][0] ^= v.x;
+        xb[m][1] ^= v.y;
+        xb[m][2] ^= v.z;
+        xb[m][3] ^= v.w;
+        stw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+      }
+  if constexpr (NN > 0) {
+    uint32_t ob[NN][W];
+#pragma unroll
+    for (int u = 0; u < NN; ++u) {
+      const uint4 v = xfer[kStOut + u][t];
+      ob[u][0] = v.x;
+      ob[u][1] = v.y;
+      ob[u][2] = v.z;
+      ob[u][3] = v.w;
+    }
+    // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
+#pragma unroll
+    for (int m = 0; m < kStSrc; m += 2) {
+      if (m + 1 < nd) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+      else if (m < nd) rows_mac1<NN, W>(ob, a.bt[m], xb[m]);
+    }
+#pragma unroll
+    for (int u = 0; u < NN; ++u)
+      if (u < a.nn) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
+  }
+}
+
 // ============================================================ update_rows kernel
 // Update with a per-stripe data row (xrs_plan.h UpdRowsPlan).  The row's
 // coefficient tables are read from the kernel arguments with a per-lane index
@@ -1067,7 +1171,7 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // overall; profiles/r02_staged_ws.log).  XRS_STAGED_WS=0 / 64 / 128 /
       // 256 / 512 / 128o5 forces it off or a block size (A/B, tests).
       const char* wv = std::getenv("XRS_STAGED_WS");
-      if (!wv || !*wv) {
+      if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {
         if (NL <= 3) return launch_staged_ws<NL, NN, 256>(a, p, stream);
       } else {
         if (std::strcmp(wv, "128") == 0) return launch_staged_ws<NL, NN, 128>(a, p, stream);
@@ -1078,6 +1182,25 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       }
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
+    }
+  }
+  if constexpr (VEC) {
+    // Runtime-count wave-specialised kernel for one lost and needed vect
+    // with parity in the pattern (12+4, lost P12 / P13: +3.4 / +1.3% at 4 KiB,
+    // +3.3 / +0.2% at 1 MiB).  With more outputs it wins or loses by pattern
+    // (12+4 lost {0, 13}: +8% at 4 KiB, -2% at 1 MiB) and loses 3-10% on
+    // lost data at 10+4 and 6+3, so the one-wave late kernel stays there
+    // (profiles/r02_staged_ws_rt.log).  XRS_STAGED_WS=rt forces it for every
+    // runtime-count launch, =0 never.
+    const char* wv = std::getenv("XRS_STAGED_WS");
+    const bool ws_rt = (wv && *wv) ? std::strcmp(wv, "rt") == 0 : (NL == 1 && NN == 1);
+    if (late && ws_rt) {
+      constexpr int T = 256;
+      const uint64_t wblocks = (a.total + T - 1) / T;
+      a.order = block_order(Shape::kStaged, true, p.half, wblocks, T);
+      hipLaunchKernelGGL((staged_ws_rt_kernel<NL, NN, T>), dim3(static_cast<unsigned>(wblocks)),
+                         dim3(2 * T), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
     }
   }
   if (late)

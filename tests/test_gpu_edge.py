@@ -153,12 +153,17 @@ def test_reconst_random_both_paths(rng, reconst_mode, size):
             assert np.array_equal(a[i], b[i]), (reconst_mode, lost, need, i)
 
 
-@pytest.mark.parametrize("d,p", [(10, 4), (6, 3), (4, 2), (14, 2), (3, 9)])
+@pytest.mark.parametrize("d,p", [(10, 4), (6, 3), (4, 2), (14, 2), (3, 9), (16, 4), (15, 5),
+                                 (16, 6)])
 def test_reconst_other_configs_both_paths(rng, reconst_mode, d, p):
+    """Per-stripe Reconst on other codecs; 16+4 / 15+5 read more than 16
+    b-rows (the wide wave-specialised kernel), 16+6 has five retrieveRS rows,
+    and 1,030-B vects have a ragged end (both run the step plan)."""
     x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
-    for _ in range(20):
-        v = [rng.integers(0, 256, size=1024, dtype=np.uint8) for _ in range(d)]
-        v += [np.zeros(1024, np.uint8) for _ in range(p)]
+    for it in range(20):
+        size = 1030 if it % 4 == 3 else 1024
+        v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(d)]
+        v += [np.zeros(size, np.uint8) for _ in range(p)]
         o.encode(v)
         lost = [int(t) for t in rng.permutation(d + p)[: int(rng.integers(1, p + 1))]]
         need = lost[: int(rng.integers(0, len(lost) + 1))]
@@ -234,7 +239,7 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
 
 
 @pytest.mark.parametrize("ws", ["", "0", "rt"])
-@pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4)])
+@pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4), (15, 5)])
 @pytest.mark.parametrize("size,n", [(4096, 520), (1 << 20, 4)])
 def test_reconst_batched_runtime_shapes_vs_oracle(rng, monkeypatch, ws, d, p, size, n):
     """General Reconst on full grids through the runtime-count staged kernels

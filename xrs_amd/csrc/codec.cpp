@@ -352,7 +352,7 @@ int reconst_staged(const xrs_codec* x, const Layout& L, size_t size, size_t n_st
   for (int h = d + 1; h < n; ++h) {  // xrs.go:305-320: h in dpHas, h > d
     if (!in_has[h] || x->xs[h].empty()) continue;
     if (bpos[h] < 0) {
-      if (plan.nb == xrs::kStSrc) return 1;
+      if (plan.nb == xrs::kStB) return 1;
       bpos[h] = plan.nb;
       plan.bsrc[plan.nb++] = L.row(h, half);
     }
@@ -368,7 +368,11 @@ int reconst_staged(const xrs_codec* x, const Layout& L, size_t size, size_t n_st
   if (!fits) return 1;
   plan.half = half;
   plan.n_stripes = n_stripes;
-  if (half > 0 && n_stripes > 0 && xrs::launch_staged(plan, s) != 0) return XRS_ERR_HIP;
+  if (half > 0 && n_stripes > 0) {
+    const int e = xrs::launch_staged(plan, s);
+    if (e == xrs::kStagedDecline) return 1;  // nothing launched: the step plan runs
+    if (e != 0) return XRS_ERR_HIP;
+  }
   for (int t : a_lost) w->add(t, 0);
   for (int h = d + 1; h < n; ++h)
     if (in_has[h] && !x->xs[h].empty()) w->add(h, 1);

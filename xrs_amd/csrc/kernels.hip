@@ -446,9 +446,9 @@ template <int NL, int NN, bool VEC>
 struct StagedArgs {
   GfTab at[kStSrc][NL > 0 ? NL : 1];
   GfTab bt[kStSrc][NN > 0 ? NN : 1];
-  RowRef asrc[kStSrc], bsrc[kStSrc];
+  RowRef asrc[kStSrc], bsrc[kStB];
   RowRef adst[kStOut], bdst[kStOut];
-  uint32_t bret[kStSrc];
+  uint32_t bret[kStB];
   uint32_t nmask[kStOut];
   uint32_t rmask[kStOut];  // the nonzero bret[] entries, compacted (late variant)
   int rb[kStOut];          // ... and their b-row indexes
@@ -832,7 +832,7 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
 // vmcnt(0) the waitcnt pass puts after guarded loads costs no extra round
 // trip).  Same conditions as staged_late_kernel: every retrieveRS row is
 // written back and there are at most kStOut of them.
-template <int NL, int NN, int T>
+template <int NL, int NN, int T, int NBM = kStSrc>
 __global__ __launch_bounds__(2 * T) void staged_ws_rt_kernel(const StagedArgs<NL, NN, true> a) {
   constexpr int W = 4;
   constexpr int L1 = NL > 0 ? NL : 1, N1 = NN > 0 ? NN : 1;
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(2 * T) void staged_ws_rt_kernel(const StagedArgs<NL
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
   const int nd = a.nd;
-  uint32_t xb[kStSrc][W];
+  uint32_t xb[NBM][W];
   if (!blane) {
     if (valid) {
       uint32_t xa[kStSrc][W], al[L1][W];
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(2 * T) void staged_ws_rt_kernel(const StagedArgs<NL
   } else if (valid) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int m = 0; m < kStSrc; ++m)
+    for (int m = 0; m < NBM; ++m)
       if (m < a.nb) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
     __builtin_amdgcn_s_setprio(0);
   }
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(2 * T) void staged_ws_rt_kernel(const StagedArgs<NL
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   if (!blane || !valid) return;
 #pragma unroll
-  for (int m = 0; m < kStSrc; ++m)
+  for (int m = 0; m < NBM; ++m)
 #pragma unroll
     for (int r = 0; r < kStOut; ++r)
       if (r < a.nr && a.rb[r] == m) {
@@ -1094,6 +1094,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     for (int q = 0; q < NL; ++q) a.at[m][q] = gf.tab(p.acoef[m][q]);
     for (int u = 0; u < NN; ++u) a.bt[m][u] = gf.tab(p.bcoef[m][u]);
     a.asrc[m] = p.asrc[m];
+  }
+  for (int m = 0; m < kStB; ++m) {
     a.bsrc[m] = p.bsrc[m];
     a.bret[m] = p.bret[m];
   }
@@ -1105,7 +1107,7 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   a.bstore = p.bstore;
   a.nr = 0;
   bool late = true;
-  for (int m = 0; m < kStSrc; ++m) {
+  for (int m = 0; m < kStB; ++m) {
     if (!p.bret[m]) continue;
     if (a.nr == kStOut || !((p.bstore >> m) & 1u)) {
       late = false;
@@ -1132,6 +1134,23 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   // CU is latency-bound: there the all-loads-first kernel pays one memory
   // round trip instead of two (a per-stripe call on host-mapped staging: one
   // PCIe round trip).  XRS_STAGED_LATE=0 / =1 forces either kernel.
+  if (p.nb > kStSrc) {
+    // Wide b-side (launch_staged checked: aligned, no ragged end, every
+    // retrieveRS row written back, at most kStOut of them): only the
+    // wave-specialised kernel holds kStB b-rows, on any grid.
+    if constexpr (VEC) {
+      if (!late) return kStagedDecline;
+      constexpr int T = 256;
+      const uint64_t wblocks = (a.total + T - 1) / T;
+      a.order = block_order(Shape::kStaged, true, p.half, wblocks, T);
+      (void)hipGetLastError();
+      hipLaunchKernelGGL((staged_ws_rt_kernel<NL, NN, T, kStB>), dim3(static_cast<unsigned>(wblocks)),
+                         dim3(2 * T), 0, stream, a);
+      return static_cast<int>(hipGetLastError());
+    } else {
+      return kStagedDecline;
+    }
+  }
   const char* lv = std::getenv("XRS_STAGED_LATE");
   if (lv && *lv) late = late && lv[0] != '0';
   else late = late && blocks >= kLatencyGrid;
@@ -1581,7 +1600,7 @@ int launch_pair(const PairPlan& p0, void* stream) {
 
 int launch_staged(const StagedPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStSrc || p0.nl < 0 ||
+  if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStB || p0.nl < 0 ||
       p0.nl > kStOut || p0.nn < 0 || p0.nn > kStOut)
     return static_cast<int>(hipErrorInvalidValue);
   bool al = true;
@@ -1589,6 +1608,17 @@ int launch_staged(const StagedPlan& p0, void* stream) {
   for (int m = 0; m < p0.nb; ++m) al = al && row_aligned(p0.bsrc[m]);
   for (int q = 0; q < p0.nl; ++q) al = al && row_aligned(p0.adst[q]);
   for (int u = 0; u < p0.nn; ++u) al = al && row_aligned(p0.bdst[u]);
+  if (p0.nb > kStSrc) {  // wide b-side: one 16-byte wave-specialised launch or none
+    const char* uv = std::getenv("XRS_UNALIGNED_VEC");  // as split_launch
+    int nr = 0;
+    bool ok = p0.half % 16 == 0 && (al || !(uv && uv[0] == '0'));
+    for (int m = 0; m < p0.nb; ++m)
+      if (p0.bret[m]) {
+        ++nr;
+        ok = ok && ((p0.bstore >> m) & 1u);
+      }
+    if (!ok || nr > kStOut) return kStagedDecline;
+  }
   return split_launch(p0, p0.half, al, [s](const StagedPlan& p, bool vec) {
     return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
   });

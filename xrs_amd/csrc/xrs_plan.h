@@ -84,15 +84,19 @@ struct RowsPlan {
 // by the RS inverse; entries past nd are extra survivors read only for XORs.
 constexpr int kStSrc = 16;
 constexpr int kStOut = 4;
+// b-rows: the d survivors plus surviving piggybacked parity past dpHas[:d]
+// (16+4: up to 19).  More than kStSrc only on the wave-specialised kernel
+// (launch_staged declines otherwise and the caller runs the step plan).
+constexpr int kStB = 20;
 
 struct StagedPlan {
   int nd;      // GF sources (d)
-  int na, nb;  // a-/b-half rows read (nd + extras), <= kStSrc
+  int na, nb;  // a-/b-half rows read (nd + extras), <= kStSrc / kStB
   int nl, nn;  // lost a-halves / needed b-halves written, <= kStOut
-  RowRef asrc[kStSrc], bsrc[kStSrc];
+  RowRef asrc[kStSrc], bsrc[kStB];
   RowRef adst[kStOut], bdst[kStOut];
   uint8_t acoef[kStSrc][kStOut], bcoef[kStSrc][kStOut];
-  uint32_t bret[kStSrc];   // abar mask XORed into b row m (0: none)
+  uint32_t bret[kStB];     // abar mask XORed into b row m (0: none)
   uint32_t bstore;         // bit m: write b row m back
   uint32_t nmask[kStOut];  // abar mask XORed into output u
   uint64_t half;
@@ -126,6 +130,10 @@ struct UpdRowsPlan {
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.
 int launch_pair(const PairPlan& plan, void* stream);
 int launch_rows(const RowsPlan& plan, void* stream);
+// kStagedDecline: the plan has more than kStSrc b-rows and cannot run as one
+// 16-byte wave-specialised launch (a ragged end, more than kStOut retrieveRS
+// rows); nothing was launched.
+constexpr int kStagedDecline = -1;
 int launch_staged(const StagedPlan& plan, void* stream);
 int launch_update_rows(const UpdRowsPlan& plan, void* stream);
 

@@ -1189,8 +1189,11 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // 64-, 128- and 512-chunk blocks and a 5-wave VGPR cap: no better
       // overall; profiles/r02_staged_ws.log).  XRS_STAGED_WS=0 / 64 / 128 /
       // 256 / 512 / 128o5 forces it off or a block size (A/B, tests).
+      // 2 lost from 512 KiB vects: 512 chunks per block (+1.2 / +2.3 / +4.2%
+      // at 1 MiB / 512 KiB / 2 MiB vects over 256; at 256 KiB vects -4%).
       const char* wv = std::getenv("XRS_STAGED_WS");
       if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {
+        if (NL == 2 && p.half >= (256u << 10)) return launch_staged_ws<NL, NN, 512>(a, p, stream);
         if (NL <= 3) return launch_staged_ws<NL, NN, 256>(a, p, stream);
       } else {
         if (std::strcmp(wv, "128") == 0) return launch_staged_ws<NL, NN, 128>(a, p, stream);

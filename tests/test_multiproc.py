@@ -80,6 +80,20 @@ def test_launch_local_split_encode_gloo(tmp_path, world, n_stripes):
     assert sum(res["counts"]) == n_stripes
 
 
+def test_rank_stdout_carries_no_gloo_noise(tmp_path):
+    """gloo's C++ side prints "[Gloo] Rank r is connected to ..." on stdout
+    while a group connects; xdist.init sends it to stderr, so rank 0's stdout
+    holds only what the program prints (bench.py: its one JSON line)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from xrs_amd import dist as x\n"
+            "sys.exit(x.launch_local(2, [sys.executable, %r, %r, '16', '64'], timeout=200))\n"
+            % (ROOT, WORKER, str(tmp_path)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Gloo" not in r.stdout, r.stdout
+    assert json.loads((tmp_path / "result.json").read_text())["ok"]
+
+
 def test_launch_local_propagates_a_failed_rank(tmp_path):
     rc = xdist.launch_local(2, [sys.executable, WORKER, str(tmp_path), "8", "64", "1"],
                             timeout=240)

@@ -27,6 +27,7 @@ import os
 import signal
 import socket
 import subprocess
+import sys
 import time
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -123,16 +124,36 @@ def launch_local(n: int, argv: Sequence[str], env=None, timeout: Optional[float]
     return rc
 
 
+class _StdoutToStderr:
+    """fd 1 -> fd 2 for the duration: gloo's C++ side prints "[Gloo] Rank r
+    is connected to ..." on stdout while the group connects, and rank 0's
+    stdout must carry only the bench's JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def init(w: World, backend: str, device=None) -> None:
-    """Join the process group (world > 1 only)."""
+    """Join the process group (world > 1 only); the first barrier connects
+    every pair, so it runs inside the stdout redirect too."""
     if w.world <= 1:
         return
     import torch.distributed as dist
 
-    if backend == "nccl":
-        dist.init_process_group("nccl", rank=w.rank, world_size=w.world, device_id=device)
-    else:
-        dist.init_process_group(backend, rank=w.rank, world_size=w.world)
+    with _StdoutToStderr():
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=w.rank, world_size=w.world, device_id=device)
+        else:
+            dist.init_process_group(backend, rank=w.rank, world_size=w.world)
+        dist.barrier()
 
 
 def finalize() -> None:

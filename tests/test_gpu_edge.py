@@ -239,7 +239,8 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
 
 
 @pytest.mark.parametrize("ws", ["", "0", "rt"])
-@pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4), (15, 5)])
+@pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4), (15, 5), (8, 4), (14, 4),
+                                 (10, 2)])
 @pytest.mark.parametrize("size,n", [(4096, 520), (1 << 20, 4)])
 def test_reconst_batched_runtime_shapes_vs_oracle(rng, monkeypatch, ws, d, p, size, n):
     """General Reconst on full grids through the runtime-count staged kernels
@@ -254,10 +255,11 @@ def test_reconst_batched_runtime_shapes_vs_oracle(rng, monkeypatch, ws, d, p, si
     o.encode_batch(host, size, n)
     s = torch.cuda.current_stream().cuda_stream
     last = d + p - 1
-    pats = [([0, 1], [0, 1]), ([d + 1], [d + 1]), ([d], [d]), ([0, d + 1], [0, d + 1]),
+    pats = [([0, 1], [0, 1]), ([0, 1, 2][:p], [0, 1, 2][:p]), ([d + 1], [d + 1]), ([d], [d]),
+            ([0, d + 1], [0, d + 1]),
             ([1, 2, last], [1, 2, last]), ([0, 1, d, d + 1][:p], [0, 1, d, d + 1][:p]),
             ([3, d + 1], [3])]
-    for lost, need in pats:
+    for lost, need in [pt for pt in pats if len(pt[0]) <= p]:  # at most p lost
         h = host.copy()
         h[:, lost] = 0xC3
         has = [i for i in range(d + p) if i not in lost]

@@ -1066,6 +1066,24 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
   return static_cast<int>(hipGetLastError());
 }
 
+// Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
+// surviving piggybacked parity past dpHas[:d]), 256 chunks per block.
+template <int ND, int NL, int NN>
+int launch_staged_ws_nd(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+  constexpr int T = 256;
+  const uint64_t blocks = (a.total + T - 1) / T;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
+  const dim3 g(static_cast<unsigned>(blocks));
+  if (p.nb == ND)
+    hipLaunchKernelGGL((staged_ws_kernel<ND, ND, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+  else if (p.nb == ND + 1)
+    hipLaunchKernelGGL((staged_ws_kernel<ND, ND + 1, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+  else
+    hipLaunchKernelGGL((staged_ws_kernel<ND, ND + 2, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 // NPRE < 0: every b-row early (NPRE = NB).
 template <int NL, int NN, int BS, int NPRE>
 int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
@@ -1158,6 +1176,28 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
   // (A compile-time survivor count, ND = 12, let the scheduler hoist the
   // b-row loads: 225-232 VGPRs plus scratch, also with a sched_barrier
   // between the a- and b-phases.  Runtime nd only.)
+  if constexpr (VEC && NL == NN && NL >= 2 && NL <= 3) {
+    // Compile-time counts for 2-3 lost data vects of d = 6, 8, 10, 14 codecs
+    // (na = nd, nb = nd..nd+2): the wave-specialised kernel.  Against the
+    // runtime one-wave late kernel (profiles/r02_staged_ws_nd.log): 4 KiB
+    // vects +4 to +12% (10+4, 8+4, 6+3, 14+4, 10+2); 1 MiB vects +2 to +4% at
+    // d = 6 and 14, -1 to -5% at d = 8 and 10, which keep the runtime kernel
+    // from 256 KiB halves.  XRS_STAGED_CT=0 / XRS_STAGED_WS=0 turn it off.
+    const char* cv = std::getenv("XRS_STAGED_CT");
+    const char* wv = std::getenv("XRS_STAGED_WS");
+    const bool big = p.half >= (256u << 10) && (p.nd == 8 || p.nd == 10);
+    const bool nd_ct = late && p.na == p.nd && p.nl == NL && p.nn == NN && p.nb >= p.nd &&
+                       p.nb <= p.nd + 2 && !big && !(cv && cv[0] == '0') && !(wv && wv[0] == '0');
+    if (nd_ct) {
+      switch (p.nd) {
+        case 6: return launch_staged_ws_nd<6, NL, NN>(a, p, stream);
+        case 8: return launch_staged_ws_nd<8, NL, NN>(a, p, stream);
+        case 10: return launch_staged_ws_nd<10, NL, NN>(a, p, stream);
+        case 14: return launch_staged_ws_nd<14, NL, NN>(a, p, stream);
+        default: break;
+      }
+    }
+  }
   if constexpr (VEC && NL == NN && NL >= 2) {
     // Compile-time counts for 12+4 losses of data vects (na = nd = 12,
     // nb = 12..14); XRS_STAGED_CT=0 keeps the runtime-count kernel (A/B).

@@ -7,7 +7,8 @@ operation (Encode, ReconstOne, Reconst with random losses and needs, Update,
 Replace).  The GPU buffer after the call must equal the oracle applied stripe
 by stripe to a host copy, byte for byte, including every byte outside the
 shards (nothing else may be written).  Seeded; bounded to a few seconds.
-XRS_FUZZ_SEEDS=N runs N seeds per test instead of 10 (long campaigns)."""
+XRS_FUZZ_SEEDS=N runs N seeds per test instead of 10 (long campaigns);
+XRS_FUZZ_BIG=1 adds 128 KiB-1 MiB vects, XRS_FUZZ_GRID=1 full grids."""
 import os
 
 import numpy as np
@@ -25,6 +26,9 @@ SEEDS = int(os.environ.get("XRS_FUZZ_SEEDS", "10"))
 
 
 BIG = os.environ.get("XRS_FUZZ_BIG") == "1"  # long campaigns: also 128 KiB-1 MiB vects
+# every other case on a grid of >= 256 blocks, where the bandwidth kernels
+# (wave-specialised staged Reconst, late / XCD-ordered launches) run
+GRID = os.environ.get("XRS_FUZZ_GRID") == "1"
 
 
 def draw_case(rng):
@@ -34,6 +38,9 @@ def draw_case(rng):
     if BIG and rng.integers(0, 4) == 0:
         size = int(rng.choice([131072, 131074, 262160, 1048576, 1048578]))
         n = int(rng.integers(1, 4))
+    if GRID and rng.integers(0, 2) == 0:
+        size = int(rng.choice([4096, 4112, 8192, 40960, 65536]))
+        n = -(-65536 * 32 // size) + int(rng.integers(0, 64))  # >= 65,536 16-byte lanes
     shard = size + int(rng.choice([0, 0, 2, 16, 256]))
     stripe = (d + p) * shard + int(rng.choice([0, 0, 6, 64]))
     base = int(rng.choice([0, 0, 0, 1, 8]))

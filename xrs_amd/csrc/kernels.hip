@@ -1068,9 +1068,8 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
 
 // Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
 // surviving piggybacked parity past dpHas[:d]), 256 chunks per block.
-template <int ND, int NL, int NN>
+template <int ND, int NL, int NN, int T = 256>
 int launch_staged_ws_nd(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
-  constexpr int T = 256;
   const uint64_t blocks = (a.total + T - 1) / T;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
@@ -1181,13 +1180,22 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     // (na = nd, nb = nd..nd+2): the wave-specialised kernel.  Against the
     // runtime one-wave late kernel (profiles/r02_staged_ws_nd.log): 4 KiB
     // vects +4 to +12% (10+4, 8+4, 6+3, 14+4, 10+2); 1 MiB vects +2 to +4% at
-    // d = 6 and 14, -1 to -5% at d = 8 and 10, which keep the runtime kernel
-    // from 256 KiB halves.  XRS_STAGED_CT=0 / XRS_STAGED_WS=0 turn it off.
+    // d = 6 and 14.  XRS_STAGED_CT=0 / XRS_STAGED_WS=0 turn it off.
     const char* cv = std::getenv("XRS_STAGED_CT");
     const char* wv = std::getenv("XRS_STAGED_WS");
-    const bool big = p.half >= (256u << 10) && (p.nd == 8 || p.nd == 10);
+    // d = 8, 10 from 256 KiB halves: 512 chunks per block (1 MiB vects, vs
+    // the runtime kernel: 10+4 +0.7 / +0.9%, 8+4 +1.4 / +5.2%; 256-chunk
+    // blocks lost 1-5% there; at 4 KiB 512 loses 2%).
+    const bool t512 = p.half >= (256u << 10) && (p.nd == 8 || p.nd == 10);
     const bool nd_ct = late && p.na == p.nd && p.nl == NL && p.nn == NN && p.nb >= p.nd &&
-                       p.nb <= p.nd + 2 && !big && !(cv && cv[0] == '0') && !(wv && wv[0] == '0');
+                       p.nb <= p.nd + 2 && !(cv && cv[0] == '0') && !(wv && wv[0] == '0');
+    if (nd_ct && t512) {
+      switch (p.nd) {
+        case 8: return launch_staged_ws_nd<8, NL, NN, 512>(a, p, stream);
+        case 10: return launch_staged_ws_nd<10, NL, NN, 512>(a, p, stream);
+        default: break;
+      }
+    }
     if (nd_ct) {
       switch (p.nd) {
         case 6: return launch_staged_ws_nd<6, NL, NN>(a, p, stream);

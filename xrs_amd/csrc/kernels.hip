@@ -1157,6 +1157,15 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     // wave-specialised kernel holds kStB b-rows, on any grid.
     if constexpr (VEC) {
       if (!late) return kStagedDecline;
+      if constexpr (NL == NN && NL >= 2 && NL <= 3) {
+        // 16+p lost data vects on full grids: the compile-time form
+        // (nb = 16..18; profiles/r02_staged_ws_nd16.log).  XRS_STAGED_CT=0
+        // keeps the runtime one.
+        const char* cv = std::getenv("XRS_STAGED_CT");
+        if (p.nd == 16 && p.na == 16 && p.nl == NL && p.nn == NN && p.nb <= 18 &&
+            blocks >= kLatencyGrid && !(cv && cv[0] == '0'))
+          return launch_staged_ws_nd<16, NL, NN>(a, p, stream);
+      }
       constexpr int T = 256;
       const uint64_t wblocks = (a.total + T - 1) / T;
       a.order = block_order(Shape::kStaged, true, p.half, wblocks, T);

@@ -1192,16 +1192,20 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     // d = 6 and 14.  XRS_STAGED_CT=0 / XRS_STAGED_WS=0 turn it off.
     const char* cv = std::getenv("XRS_STAGED_CT");
     const char* wv = std::getenv("XRS_STAGED_WS");
-    // d = 8, 10 from 256 KiB halves: 512 chunks per block (1 MiB vects, vs
-    // the runtime kernel: 10+4 +0.7 / +0.9%, 8+4 +1.4 / +5.2%; 256-chunk
-    // blocks lost 1-5% there; at 4 KiB 512 loses 2%).
-    const bool t512 = p.half >= (256u << 10) && (p.nd == 8 || p.nd == 10);
+    // From 256 KiB halves, 512 chunks per block for 2 lost, and for 3 lost at
+    // d = 8, 10 (1 MiB vects: vs the runtime kernel 10+4 +0.7 / +0.9%, 8+4
+    // +1.4 / +5.2%, where 256-chunk blocks lost 1-5%; vs 256-chunk blocks
+    // 6+3 +1.6 / -3.4%, 14+4 +3.8 / -0.3%: profiles/r02_staged_ws_nd512.log;
+    // at 4 KiB 512 loses 2%).
+    const bool t512 = p.half >= (256u << 10) && (NL == 2 || p.nd == 8 || p.nd == 10);
     const bool nd_ct = late && p.na == p.nd && p.nl == NL && p.nn == NN && p.nb >= p.nd &&
                        p.nb <= p.nd + 2 && !(cv && cv[0] == '0') && !(wv && wv[0] == '0');
     if (nd_ct && t512) {
       switch (p.nd) {
+        case 6: return launch_staged_ws_nd<6, NL, NN, 512>(a, p, stream);
         case 8: return launch_staged_ws_nd<8, NL, NN, 512>(a, p, stream);
         case 10: return launch_staged_ws_nd<10, NL, NN, 512>(a, p, stream);
+        case 14: return launch_staged_ws_nd<14, NL, NN, 512>(a, p, stream);
         default: break;
       }
     }

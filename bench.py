@@ -35,6 +35,13 @@ After the headline timed region, the same line carries:
   * "xgmi_repair" (two or more visible GPUs): rank 0 (in a child process)
     rebuilds a data shard with half of its need set on the peer GPU (xGMI
     reads), checked bit for bit against the rebuild from local shards.
+  * "parity": after the timed regions, each headline launch runs once more
+    over a batch whose first / middle / last stripes were poisoned (parity
+    for Encode, shard k in {0, 7} for ReconstOne); the checker leg compares
+    those stripes with the C oracle (oracle/xrs_oracle.c), on every rank;
+  * "rank_devices": every rank's device index and PCI address.  Two ranks on
+    one GPU stop the run (exit 3) unless XRS_REHEARSAL=1, which labels the
+    line "shared_gpu": true.
 
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
 """
@@ -147,15 +154,105 @@ def cpu_baseline(seconds: float, step_bytes: dict):
     }
 
 
-def pmc_traffic(kernel_key: str):
-    """HBM bytes per launch from profiles/pmc_traffic.json (written by
-    tools/pmc_traffic.py from rocprofv3 --pmc passes), or None."""
+def lib_sha256(path: str) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def pmc_traffic(launch: str, kernel: str, lib_path: str):
+    """(HBM bytes per launch, provenance) from profiles/pmc_traffic.json
+    (tools/pmc_traffic.py over two rocprofv3 --pmc passes of this bench).  An
+    entry counts only when it names this launch, this kernel and the sha256
+    of the library this process loaded: after any rebuild the stored counters
+    describe other code, and the line reports traffic null."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(kernel_key, {}).get("hbm_bytes_per_launch")
+            ent = json.load(f).get(launch)
+        sha = lib_sha256(lib_path)
     except (OSError, ValueError):
-        return None
+        return None, "profiles/pmc_traffic.json unreadable"
+    if not isinstance(ent, dict):
+        return None, f"no PMC entry for {launch}"
+    if ent.get("kernel") != kernel:
+        return None, f"PMC entry is for kernel {ent.get('kernel')!r}, not {kernel!r}"
+    if ent.get("lib_sha256") != sha:
+        return None, (f"PMC entry measured library sha256 {str(ent.get('lib_sha256'))[:12]}, "
+                      f"loaded library is {sha[:12]}")
+    return ent.get("hbm_bytes_per_launch"), (
+        f"profiles/pmc_traffic.json[{launch}]: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+        f"this bench, library sha256 {sha[:12]} (the loaded one)")
+
+
+# ---------------------------------------------------------------- parity leg
+# Driver-visible bit-exactness: after the timed regions, each headline launch
+# runs once more (full grid, same kernel shape) over a batch whose sample
+# stripes were poisoned first; the sample stripes' bytes before and after come
+# back to the host, and the checker leg (with cpu_baseline, never timed)
+# compares them with the C oracle.  Reference semantics: Encode xrs.go:103-128,
+# ReconstOne xrs.go:175-221.
+PARITY_K = (0, 7)
+
+
+def parity_capture(R: "Rank", tag: str, buf, size: int, shard: int, stripe: int, n: int):
+    """GPU half of the parity leg for one vect size: returns [(key, op, k,
+    stripes, before, got)], `before` the oracle's input and `got` the GPU's
+    output for the sample stripes ([len(stripes), D+P, size] uint8)."""
+    torch, x, s = R.torch, R.x, R.stream
+    idx = sorted({0, n // 2, n - 1})
+    view = buf.view(n, stripe)
+
+    def grab():
+        return torch.stack([torch.stack([view[t, i * shard:i * shard + size] for i in range(D + P)])
+                            for t in idx]).cpu().numpy()
+
+    out = []
+    for t in idx:  # Encode: parity of the samples poisoned, then a full launch
+        for i in range(D, D + P):
+            view[t, i * shard:i * shard + size].fill_(0xA5)
+    R.sync()
+    before = grab()
+    x.encode_batched(buf.data_ptr(), size, shard, stripe, n, s)
+    R.sync()
+    out.append(("encode_" + tag, "encode", -1, idx, before, grab()))
+    for k in PARITY_K:  # ReconstOne k: shard k of the samples poisoned
+        for t in idx:
+            view[t, k * shard:k * shard + size].fill_(0x5A)
+        R.sync()
+        before = grab()
+        x.reconst_one_batched(buf.data_ptr(), size, shard, stripe, n, k, s)
+        R.sync()
+        out.append(("reconst_one_" + tag, "reconst_one", k, idx, before, grab()))
+    return out
+
+
+def oracle_parity(samples):
+    """Checker half of the parity leg: the C oracle (oracle/xrs_oracle.c) on
+    each sample's `before`, compared byte for byte with the GPU's output."""
+    import numpy as np
+
+    from oracle.oracle_c import OracleXRS
+
+    o = OracleXRS(D, P)
+    res = {"oracle": "oracle/xrs_oracle.c", "cases": []}
+    for key, op, k, idx, before, got in samples:
+        ref = before.copy()
+        for j in range(ref.shape[0]):
+            vects = [ref[j, i] for i in range(D + P)]
+            if op == "encode":
+                o.encode(vects)
+            else:
+                o.reconst_one(vects, k)
+        ok = bool(np.array_equal(ref, got))
+        res[key] = res.get(key, True) and ok
+        res["cases"].append({"launch": key, "k": None if k < 0 else k, "stripes": idx,
+                             "vect_bytes": int(before.shape[2]), "bitexact": ok})
+    return res
 
 
 def parse_args(argv=None):
@@ -178,8 +275,13 @@ def parse_args(argv=None):
                     help="1 MiB stripes for the xgmi_repair key (0: skip)")
     ap.add_argument("--xgmi-child", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--ramp-seconds", type=float, default=0.5)
+    # Untimed soak of the headline Encode before the warmup: clock ramp, and
+    # >= 6 s of GPU work so a sampler polling GPU busy every few seconds sees
+    # the run whatever --steps is.
+    ap.add_argument("--ramp-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the post-timing oracle parity leg")
     return ap.parse_args(argv)
 
 
@@ -195,10 +297,22 @@ class Rank:
         self.ndev = torch.cuda.device_count()
         if self.ndev < 1:
             raise RuntimeError("bench.py needs a GPU (there is no CPU fallback)")
+        self.rehearsal = xdist.rehearsal_env()
+        # local rank -> visible device; with fewer devices than ranks the PCI
+        # check below refuses the run unless it is a labelled rehearsal (a
+        # launcher that gives each rank its own single visible GPU passes it)
         self.dev_index = w.local % self.ndev
         torch.cuda.set_device(self.dev_index)
         self.dev = torch.device("cuda", self.dev_index)
         xdist.init(w, backend, self.dev)
+        pr = torch.cuda.get_device_properties(self.dev_index)
+        me = {"rank": w.rank, "device": self.dev_index,
+              "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+              "uuid": str(getattr(pr, "uuid", ""))}
+        # every rank's device, checked distinct by PCI address (XRS_REHEARSAL=1
+        # allows sharing and labels the line)
+        self.rank_devices = xdist.gather_objects(me)
+        self.shared_gpu = xdist.check_distinct_devices(self.rank_devices, self.rehearsal)
         # the time gather runs on the device for RCCL, on the host for gloo
         self.tdev = self.dev if (w.world > 1 and backend == "nccl") else None
         self.x = xrs_amd.XRS(D, P)
@@ -248,18 +362,19 @@ def headline(R: Rank, args):
     R.sync()
     R.ramp(lambda: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s),
            args.ramp_seconds)
-    # The four timed launches of a step, in order: (key, kernel, algorithmic
-    # bytes per launch, read bytes per launch, launcher).
+    # The four timed launches of a step, in order: (key, expected kernel,
+    # algorithmic bytes per launch, read bytes per launch, launcher).  The
+    # line reports the kernel the library actually launched (traced below).
     launches = [
-        ("encode_4k", "pair_kernel<4,12,false,true,128,false>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
+        ("encode_4k", "pair_kernel<4, 12, false, true, 128, false>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
          lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s)),
-        ("reconst_one_4k", "rows_kernel<2,12,4,false,true,256>", n_enc * 9 * ENC_S,
+        ("reconst_one_4k", "rows_kernel<2, 12, 4, false, true, 256>", n_enc * 9 * ENC_S,
          n_enc * 8 * ENC_S,
          lambda i: x.reconst_one_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc,
                                          i % D, s)),
-        ("encode_1m", "pair_kernel<4,12,false,true,128,true>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
+        ("encode_1m", "pair_kernel<4, 12, false, true, 128, true>", n_rec * (D + P) * REC_S, n_rec * D * REC_S,
          lambda i: x.encode_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec, s)),
-        ("reconst_one_1m", "rows_kernel<2,12,4,false,true,1024>", n_rec * 9 * REC_S,
+        ("reconst_one_1m", "rows_kernel<2, 12, 4, false, true, 1024>", n_rec * 9 * REC_S,
          n_rec * 8 * REC_S,
          lambda i: x.reconst_one_batched(rec_buf.data_ptr(), REC_S, rec_shard, rec_stripe, n_rec,
                                          i % D, s)),
@@ -280,6 +395,14 @@ def headline(R: Rank, args):
             events[nl].record()
             state["i"] += 1
 
+    # The kernel each launch runs, read from the library's launch trace
+    # (one untimed call each): the names rocprofv3 reports.
+    traced = {}
+    for key, _, _, _, fn in launches:
+        R.xrs_amd.trace_kernels(True)
+        fn(0)
+        R.xrs_amd.trace_kernels(False)
+        traced[key] = "; ".join(R.xrs_amd.traced_kernels()) or "?"
     # warmup steps untimed, then exactly args.steps timed ones (with events)
     for i in range(args.warmup):
         step(i)
@@ -287,19 +410,25 @@ def headline(R: Rank, args):
     rank_seconds = R.timed(step, args.steps, 0)
 
     kernels = {}
-    for j, (key, kname, nbytes, rbytes, _) in enumerate(launches):
+    for j, (key, _, nbytes, rbytes, _) in enumerate(launches):
         ms = sum(e[j].elapsed_time(e[j + 1]) for e in ev) / len(ev)
         kernels[key] = {
-            "kernel": kname, "ms": round(ms, 4), "bytes_per_launch": nbytes,
+            "kernel": traced[key], "ms": round(ms, 4), "bytes_per_launch": nbytes,
             "gibps": round(nbytes / (ms / 1e3) / GIB, 1),
             "achieved_gbs": round(nbytes / (ms / 1e3) / 1e9, 1),
             "frac": round(nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "read_only_gbs": round(rbytes / (ms / 1e3) / 1e9, 1),
             "read_frac": round(rbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+    samples = []
+    if not args.no_parity:  # untimed: the timed region has ended on every rank
+        if n_enc > 0:
+            samples += parity_capture(R, "4k", enc_buf, ENC_S, enc_shard, enc_stripe, n_enc)
+        if n_rec > 0:
+            samples += parity_capture(R, "1m", rec_buf, REC_S, rec_shard, rec_stripe, n_rec)
     del enc_buf, rec_buf
     torch.cuda.empty_cache()
-    return launches, step_bytes, rank_seconds, kernels, (enc_shard, rec_shard)
+    return launches, step_bytes, rank_seconds, kernels, (enc_shard, rec_shard), samples
 
 
 def config5(R: Rank, args):
@@ -513,17 +642,18 @@ def run_rank(args, w):
     # runs the same bracket over RCCL instead.
     backend = os.environ.get("XRS_DIST_BACKEND", "gloo")
     R = Rank(w, backend)
-    launches, step_bytes, rank_seconds, kernels, strides = headline(R, args)
+    launches, step_bytes, rank_seconds, kernels, strides, samples = headline(R, args)
     elapsed_max = max(rank_seconds)
     value = w.world * args.steps * step_bytes / elapsed_max / GIB
 
     dom_key = max(kernels, key=lambda k: kernels[k]["ms"])
     dom = kernels[dom_key]
+    traffic, traffic_source = pmc_traffic(dom_key, dom["kernel"], R.xrs_amd.LIB_PATH)
     roofline = {
         "bound": "hbm", "kernel": dom["kernel"], "launch": dom_key,
         "achieved": dom["achieved_gbs"],
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom["achieved_gbs"] / HBM_PEAK_GBS, 4),
-        "traffic": pmc_traffic(dom_key),
+        "traffic": traffic, "traffic_source": traffic_source,
         "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
         # the north star's "HBM-read roofline": read bytes only over the same
         # peak (DESIGN.md §5 explains why 0.70 of it is out of reach for a
@@ -543,6 +673,16 @@ def run_rank(args, w):
             xg = run_xgmi_child(args, R.dev_index, R.ndev)
         xdist.barrier()
 
+    # Checker leg (untimed): the oracle on every rank's parity samples, then
+    # the CPU baseline on rank 0 at N = 1.
+    parity = None
+    if samples:
+        log("oracle parity of the sampled stripes ...")
+        mine = oracle_parity(samples)
+        oks = [v > 0.5 for v in xdist.gather_seconds(
+            1.0 if all(c["bitexact"] for c in mine["cases"]) else 0.0, R.tdev)]
+        parity = dict(mine, all_ranks=oks, bitexact=all(oks))
+        del samples
     cpu = None
     if w.rank == 0 and w.world == 1 and not args.no_cpu_baseline:
         log("timing CPU baseline ...")
@@ -574,8 +714,11 @@ def run_rank(args, w):
                 "parallelism": f"stripe split x{w.world}, no collective",
             },
             "rank_seconds": [round(v, 6) for v in rank_seconds],
+            "rank_devices": R.rank_devices,
+            "shared_gpu": R.shared_gpu,
             "kernels": kernels,
             "roofline": roofline,
+            "parity": parity,
             "cpu_baseline": cpu,
             "config5": c5,
             "host_e2e": he,
@@ -600,7 +743,11 @@ def main(argv=None):
         # before this process makes any GPU call, and exit with their status.
         argv = sys.argv[1:] if argv is None else list(argv)
         return xdist.launch_local(w.world, [sys.executable, os.path.abspath(__file__)] + argv)
-    return run_rank(args, w)
+    try:
+        return run_rank(args, w)
+    except xdist.SharedDevice as e:
+        log(f"bench.py: {e}")
+        return 3
 
 
 if __name__ == "__main__":

@@ -53,6 +53,13 @@ const char *xrs_strerror(int code);
 int xrs_format_error(int code, long long arg, char *buf, size_t buflen);
 /* Library version string, and the gfx target the kernels were built for. */
 const char *xrs_version(void);
+/* Diagnostics (no reference counterpart): record which kernel instantiations
+ * the library launches, process-wide.  xrs_trace_kernels(1) clears the record
+ * and starts it, (0) stops it.  xrs_traced_kernels writes one "name count"
+ * line per kernel, in first-launch order, NUL-terminated and truncated to
+ * cap, and returns the full length.  smoke() and the dispatch tests use it. */
+int xrs_trace_kernels(int on);
+size_t xrs_traced_kernels(char *buf, size_t cap);
 
 /* ---- codec ----------------------------------------------------------- */
 /* xrs.go:55 New(dataNum, parityNum).  Builds the systematic Cauchy generator

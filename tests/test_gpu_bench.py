@@ -14,10 +14,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SMALL = ["--steps", "3", "--warmup", "1", "--enc-stripes", "2048", "--rec-stripes", "16",
          "--no-cpu-baseline", "--config5-stripes", "64", "--config5-steps", "2", "--host-mib", "32",
-         "--xgmi-stripes", "4"]
+         "--xgmi-stripes", "4", "--ramp-seconds", "0.3"]
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
-        "cpu_baseline"}
+        "cpu_baseline", "parity", "rank_devices", "shared_gpu"}
+PARITY_KEYS = ("encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m")
+
+
+def _check_parity(j):
+    """The line's oracle parity leg: every headline launch bit-exact on its
+    sampled stripes (first / middle / last), ReconstOne at two k."""
+    par = j["parity"]
+    assert par["oracle"] == "oracle/xrs_oracle.c"
+    assert all(par[k] is True for k in PARITY_KEYS), par
+    assert par["bitexact"] is True and all(par["all_ranks"])
+    assert len(par["cases"]) == 6 and all(c["bitexact"] for c in par["cases"])
 
 
 def _line(out: str) -> dict:
@@ -41,6 +52,8 @@ def test_bench_one_gpu_contract():
     assert j["n_gpus"] == 1 and j["steps"] == 3 and j["value"] > 0
     assert j["roofline"]["bound"] == "hbm" and 0 < j["roofline"]["frac"] < 1
     assert set(j["kernels"]) == {"encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m"}
+    _check_parity(j)
+    assert j["shared_gpu"] is False and len(j["rank_devices"]) == 1
     c5 = j["config5"]
     assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok"]
     assert len(c5["encode"]["rank_seconds"]) == 1 and c5["gibps"] > 0
@@ -63,8 +76,22 @@ def test_bench_xgmi_child_self_peer():
     assert xg["gbs_algorithmic"] > 0 and xg["gbs_all_local"] > 0
 
 
+def test_bench_two_ranks_refused_on_one_card():
+    """Two ranks on a one-GPU box without XRS_REHEARSAL: bench.py refuses
+    (exit 3) instead of printing a line that claims two GPUs."""
+    import torch
+    if torch.cuda.device_count() > 1:
+        pytest.skip("two GPUs visible: the ranks would not share a card")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "XRS_REHEARSAL")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 3, r.stderr[-3000:]
+    assert "same GPU" in r.stderr and not r.stdout.strip()
+
+
 def test_bench_two_ranks_contract():
-    env = dict(os.environ)
+    env = dict(os.environ, XRS_REHEARSAL="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
@@ -80,6 +107,14 @@ def test_bench_two_ranks_contract():
     assert c5["stripes_total"] == 128 and c5["roundtrip_ok"] and len(c5["roundtrip_ok_ranks"]) == 2
     assert len(j["config5"]["reconst_one"]["rank_seconds"]) == 2
     assert len(j["host_e2e"]["encode_4k"]["rank_gibps"]) == 2
+    _check_parity(j)
+    assert len(j["rank_devices"]) == 2
+    assert j["shared_gpu"] is (torch_device_count() < 2)
+
+
+def torch_device_count():
+    import torch
+    return torch.cuda.device_count()
 
 
 def test_bench_self_launch_two_ranks():
@@ -87,6 +122,7 @@ def test_bench_self_launch_two_ranks():
     form the driver may use); on a one-GPU box they share cuda:0 over gloo."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["XRS_REHEARSAL"] = "1"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]

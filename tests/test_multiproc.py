@@ -101,6 +101,44 @@ def test_launch_local_propagates_a_failed_rank(tmp_path):
     assert not (tmp_path / "result.json").exists()
 
 
+DEV_WORKER = os.path.join(ROOT, "tests", "_device_worker.py")
+
+
+def test_check_distinct_devices():
+    a = {"rank": 0, "pci": "0000:05:00"}
+    b = {"rank": 1, "pci": "0000:15:00"}
+    assert xdist.check_distinct_devices([a, b], rehearsal=False) is False
+    same = dict(b, pci=a["pci"])
+    with pytest.raises(xdist.SharedDevice, match="ranks 0 and 1"):
+        xdist.check_distinct_devices([a, same], rehearsal=False)
+    assert xdist.check_distinct_devices([a, same], rehearsal=True) is True
+    assert xdist.rehearsal_env({"XRS_REHEARSAL": "1"}) and not xdist.rehearsal_env({})
+    assert not xdist.rehearsal_env({"XRS_REHEARSAL": "0"})
+
+
+@pytest.mark.parametrize("pcis,rehearsal,rc,shared", [
+    ("0000:05:00,0000:15:00", False, 0, False),     # two GPUs: fine
+    ("0000:05:00,0000:05:00", False, 3, None),      # one card, no label: refused
+    ("0000:05:00,0000:05:00", True, 0, True),       # labelled rehearsal
+])
+def test_rank_devices_gloo(tmp_path, pcis, rehearsal, rc, shared):
+    """The start-up gather of every rank's GPU over gloo, world size 2: a
+    layout where two ranks share a card exits 3 (bench.py's status) unless
+    XRS_REHEARSAL=1, and then says shared."""
+    env = dict(os.environ, XRS_TEST_PCI=pcis)
+    env.pop("XRS_REHEARSAL", None)
+    if rehearsal:
+        env["XRS_REHEARSAL"] = "1"
+    got = xdist.launch_local(2, [sys.executable, DEV_WORKER, str(tmp_path)], env=env, timeout=200)
+    assert got == rc
+    if rc == 0:
+        res = json.loads((tmp_path / "result.json").read_text())
+        assert res["shared"] is shared
+        assert [d["pci"] for d in res["devices"]] == pcis.split(",")
+    else:
+        assert "same GPU" in (tmp_path / "refused.txt").read_text()
+
+
 def test_launch_local_sigterm_stops_the_ranks(tmp_path):
     """SIGTERM to the launching parent stops every rank it started (a
     driver's time limit must not leave ranks holding GPUs)."""

@@ -5,7 +5,10 @@
         python bench.py --steps 3 --warmup 1 --no-cpu-baseline
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- \
         python bench.py --steps 3 --warmup 1 --no-cpu-baseline
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [LIB] > profiles/pmc_traffic.json
+
+Each entry carries the kernel instantiation and the sha256 of the library
+(LIB, default xrs_amd/libxrs_hip.so) the passes ran.
 
 Corrections (/opt/skills/guides/MI355X_MICROARCH.md "HBM"): FETCH_SIZE and
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a
@@ -15,6 +18,7 @@ launches are told apart from the setup encode by grid size.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -46,8 +50,19 @@ def read_counter(d, counter):
     return vals
 
 
+def lib_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
 def main():
     fetch_dir, write_dir = sys.argv[1], sys.argv[2]
+    lib = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "xrs_amd", "libxrs_hip.so")
+    sha = lib_sha256(lib)
     fetch = read_counter(fetch_dir, "FETCH_SIZE")
     write = read_counter(write_dir, "WRITE_SIZE")
     out = {}
@@ -57,6 +72,9 @@ def main():
         f = sum(fetch[key]) / len(fetch[key]) * 1024 * 2  # KiB, gfx950 half-count
         w = sum(write[key]) / len(write[key]) * 1024
         out[key] = {
+            # provenance: bench.py attaches these counters only when its
+            # dominant launch ran this kernel from this very library build
+            "kernel": KERNELS[key][0], "lib_sha256": sha,
             "fetch_bytes_per_launch": int(f), "write_bytes_per_launch": int(w),
             "hbm_bytes_per_launch": int(f + w),
             "algorithmic_bytes_per_launch": ALGO_BYTES[key],

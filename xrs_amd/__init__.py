@@ -17,7 +17,8 @@ import ctypes
 import os
 import threading
 
-__all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes"]
+__all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes",
+           "trace_kernels", "traced_kernels"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # XRS_LIB: an alternative build of the library (A/B experiments only).
@@ -71,6 +72,8 @@ def _load():
         "xrs_strerror": ([I], ctypes.c_char_p),
         "xrs_format_error": ([I, ctypes.c_longlong, ctypes.c_char_p, Z], I),
         "xrs_version": ([], ctypes.c_char_p),
+        "xrs_trace_kernels": ([I], I),
+        "xrs_traced_kernels": ([ctypes.c_char_p, Z], Z),
         "xrs_new": ([I, I, ctypes.POINTER(P)], I),
         "xrs_free": ([P], None),
         "xrs_data_num": ([P], I),
@@ -186,6 +189,24 @@ def batch_strides(size: int, n_shards: int):
     a, b = ctypes.c_size_t(), ctypes.c_size_t()
     _raise(_lib.xrs_batch_strides(size, n_shards, ctypes.byref(a), ctypes.byref(b)))
     return a.value, b.value
+
+
+def trace_kernels(on: bool = True) -> None:
+    """Start (clearing the record) or stop recording the kernels the library
+    launches (xrs_trace_kernels; diagnostics)."""
+    _lib.xrs_trace_kernels(1 if on else 0)
+
+
+def traced_kernels() -> dict:
+    """{kernel instantiation: launches} recorded since trace_kernels(True)."""
+    n = _lib.xrs_traced_kernels(None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib.xrs_traced_kernels(buf, n + 1)
+    out = {}
+    for ln in buf.value.decode().splitlines():
+        name, _, cnt = ln.rpartition(" ")
+        out[name] = int(cnt)
+    return out
 
 
 def _raise(code: int, arg: int = 0):

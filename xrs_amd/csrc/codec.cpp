@@ -905,6 +905,13 @@ int xrs_format_error(int code, long long arg, char* buf, size_t buflen) {
 
 const char* xrs_version(void) { return "xrs-hip 0.1 gfx950"; }
 
+int xrs_trace_kernels(int on) {
+  xrs::trace_kernels(on != 0);
+  return XRS_OK;
+}
+
+size_t xrs_traced_kernels(char* buf, size_t cap) { return xrs::traced_kernels(buf, cap); }
+
 // xrs.go:55-68 New + makeXORSet :77-100
 int xrs_new(int data_num, int parity_num, xrs_codec** out) {
   if (!out) return XRS_ERR_INVALID_ARG;

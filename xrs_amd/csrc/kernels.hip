@@ -22,9 +22,15 @@
 //    runtime-count variants.  Misaligned / odd sizes take a byte-granular path.
 #include <hip/hip_runtime.h>
 
+#include <cxxabi.h>
+
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <utility>
+#include <vector>
 
 #include "gf256.h"
 #include "xrs_plan.h"
@@ -990,6 +996,64 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P
   }
 }
 
+// ============================================================ launch trace
+// Diagnostic record of which kernel instantiations this process launched
+// (xrs_trace_kernels / xrs_traced_kernels): smoke() and the dispatch tests
+// name the kernels they exercised.  Off: one relaxed atomic load per launch.
+std::atomic<bool> g_trace{false};
+std::mutex g_trace_mu;
+std::vector<std::pair<std::string, uint64_t>> g_trace_log;  // (kernel, launches)
+
+// Device symbol name -> "pair_kernel<4, 12, false, true, 128, true>" (the
+// name rocprofv3 prints, without namespaces, return type and parameters).
+std::string clean_kernel_name(const char* sym) {
+  if (!sym) return "?";
+  std::string n(sym);
+  int st = 0;
+  if (char* dm = abi::__cxa_demangle(sym, nullptr, nullptr, &st)) {
+    n = dm;
+    std::free(dm);
+  }
+  if (n.compare(0, 5, "void ") == 0) n.erase(0, 5);
+  for (const char* ns : {"xrs::(anonymous namespace)::", "(anonymous namespace)::", "xrs::"})
+    for (size_t i; (i = n.find(ns)) != std::string::npos;) n.erase(i, std::strlen(ns));
+  int depth = 0;  // drop the parameter list: the first '(' outside <...>
+  for (size_t i = 0; i < n.size(); ++i) {
+    if (n[i] == '<') ++depth;
+    else if (n[i] == '>') --depth;
+    else if (n[i] == '(' && depth == 0) {
+      n.resize(i);
+      break;
+    }
+  }
+  return n;
+}
+
+template <auto K>
+const char* kernel_name(hipStream_t s) {
+  static const std::string n =
+      clean_kernel_name(hipKernelNameRefByPtr(reinterpret_cast<const void*>(K), s));
+  return n.c_str();
+}
+
+void trace_note(const char* name) {
+  std::lock_guard<std::mutex> g(g_trace_mu);
+  for (auto& e : g_trace_log)
+    if (e.first == name) {
+      ++e.second;
+      return;
+    }
+  g_trace_log.emplace_back(name, 1);
+}
+
+// hipLaunchKernelGGL with the trace hook; KERNEL is a parenthesised
+// template-id, e.g. XRS_LAUNCH((pair_kernel<4, 12, false, true>), grid, block, stream, args).
+#define XRS_LAUNCH(KERNEL, GRID, BLOCK, STREAM, ...)                                   \
+  do {                                                                                 \
+    if (g_trace.load(std::memory_order_relaxed)) trace_note(kernel_name<&KERNEL>(STREAM)); \
+    hipLaunchKernelGGL(KERNEL, GRID, BLOCK, 0, STREAM, __VA_ARGS__);                    \
+  } while (0)
+
 // ============================================================ launchers
 inline bool aligned16(uint64_t v) { return (v & 15u) == 0; }
 
@@ -1058,11 +1122,11 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
   }
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == 12)
-    hipLaunchKernelGGL((staged_ws_kernel<12, 12, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 12, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   else if (p.nb == 13)
-    hipLaunchKernelGGL((staged_ws_kernel<12, 13, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 13, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   else
-    hipLaunchKernelGGL((staged_ws_kernel<12, 14, NL, NN, T, OCC>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 14, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1075,11 +1139,11 @@ int launch_staged_ws_nd(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStre
   a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == ND)
-    hipLaunchKernelGGL((staged_ws_kernel<ND, ND, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND, NL, NN, T>), g, dim3(2 * T), stream, a);
   else if (p.nb == ND + 1)
-    hipLaunchKernelGGL((staged_ws_kernel<ND, ND + 1, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND + 1, NL, NN, T>), g, dim3(2 * T), stream, a);
   else
-    hipLaunchKernelGGL((staged_ws_kernel<ND, ND + 2, NL, NN, T>), g, dim3(2 * T), 0, stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND + 2, NL, NN, T>), g, dim3(2 * T), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1091,14 +1155,11 @@ int launch_staged_ct_bs(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStre
   a.order = block_order(Shape::kStaged, true, p.half, blocks, BS);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == 12)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 12, NL, NN, BS, NPRE < 0 ? 12 : NPRE>), g, dim3(BS),
-                       0, stream, a);
+    XRS_LAUNCH((staged_ct_kernel<12, 12, NL, NN, BS, NPRE < 0 ? 12 : NPRE>), g, dim3(BS), stream, a);
   else if (p.nb == 13)
-    hipLaunchKernelGGL((staged_ct_kernel<12, 13, NL, NN, BS, NPRE < 0 ? 13 : NPRE>), g, dim3(BS),
-                       0, stream, a);
+    XRS_LAUNCH((staged_ct_kernel<12, 13, NL, NN, BS, NPRE < 0 ? 13 : NPRE>), g, dim3(BS), stream, a);
   else
-    hipLaunchKernelGGL((staged_ct_kernel<12, 14, NL, NN, BS, NPRE < 0 ? 14 : NPRE>), g, dim3(BS),
-                       0, stream, a);
+    XRS_LAUNCH((staged_ct_kernel<12, 14, NL, NN, BS, NPRE < 0 ? 14 : NPRE>), g, dim3(BS), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1170,8 +1231,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       const uint64_t wblocks = (a.total + T - 1) / T;
       a.order = block_order(Shape::kStaged, true, p.half, wblocks, T);
       (void)hipGetLastError();
-      hipLaunchKernelGGL((staged_ws_rt_kernel<NL, NN, T, kStB>), dim3(static_cast<unsigned>(wblocks)),
-                         dim3(2 * T), 0, stream, a);
+      XRS_LAUNCH((staged_ws_rt_kernel<NL, NN, T, kStB>), dim3(static_cast<unsigned>(wblocks)),
+                         dim3(2 * T), stream, a);
       return static_cast<int>(hipGetLastError());
     } else {
       return kStagedDecline;
@@ -1281,17 +1342,17 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       constexpr int T = 256;
       const uint64_t wblocks = (a.total + T - 1) / T;
       a.order = block_order(Shape::kStaged, true, p.half, wblocks, T);
-      hipLaunchKernelGGL((staged_ws_rt_kernel<NL, NN, T>), dim3(static_cast<unsigned>(wblocks)),
-                         dim3(2 * T), 0, stream, a);
+      XRS_LAUNCH((staged_ws_rt_kernel<NL, NN, T>), dim3(static_cast<unsigned>(wblocks)),
+                         dim3(2 * T), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }
   if (late)
-    hipLaunchKernelGGL((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBlock), 0, stream, a);
+    XRS_LAUNCH((staged_late_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), stream, a);
   else
-    hipLaunchKernelGGL((staged_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBlock), 0, stream, a);
+    XRS_LAUNCH((staged_kernel<NL, NN, VEC>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1335,8 +1396,8 @@ int launch_update_rows_t(const UpdRowsPlan& p, hipStream_t stream) {
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kPair, VEC, p.half, blocks);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
-  hipLaunchKernelGGL((update_rows_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kBlock), 0, stream, a);
+  XRS_LAUNCH((update_rows_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1405,20 +1466,20 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC && P == 4 && C == 12 && !ACC) {
     if (plain12) {
-      hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC, 128, true>), dim3(static_cast<unsigned>(blocks)),
-                         dim3(128), 0, stream, a);
+      XRS_LAUNCH((pair_kernel<P, C, ACC, VEC, 128, true>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(128), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }
   if constexpr (VEC) {
     if (bs == 128) {
-      hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC, 128>), dim3(static_cast<unsigned>(blocks)),
-                         dim3(128), 0, stream, a);
+      XRS_LAUNCH((pair_kernel<P, C, ACC, VEC, 128>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(128), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }
-  hipLaunchKernelGGL((pair_kernel<P, C, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kBlock), 0, stream, a);
+  XRS_LAUNCH((pair_kernel<P, C, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1530,13 +1591,13 @@ int launch_rows_t(const RowsPlan& p, hipStream_t stream) {
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC) {
     if (bs == 1024) {
-      hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC, 1024>),
-                         dim3(static_cast<unsigned>(blocks)), dim3(1024), 0, stream, a);
+      XRS_LAUNCH((rows_kernel<R, NM, NX, ACC, VEC, 1024>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(1024), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }
-  hipLaunchKernelGGL((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kBlock), 0, stream, a);
+  XRS_LAUNCH((rows_kernel<R, NM, NX, ACC, VEC>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1644,6 +1705,26 @@ bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len) {
 }
 
 }  // namespace
+
+void trace_kernels(bool on) {
+  std::lock_guard<std::mutex> g(g_trace_mu);
+  if (on) g_trace_log.clear();
+  g_trace.store(on, std::memory_order_relaxed);
+}
+
+size_t traced_kernels(char* buf, size_t cap) {
+  std::string out;
+  {
+    std::lock_guard<std::mutex> g(g_trace_mu);
+    for (const auto& e : g_trace_log) out += e.first + " " + std::to_string(e.second) + "\n";
+  }
+  if (buf && cap) {
+    const size_t n = out.size() < cap - 1 ? out.size() : cap - 1;
+    std::memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
+  return out.size();
+}
 
 int launch_pair(const PairPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);

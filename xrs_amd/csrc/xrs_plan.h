@@ -136,5 +136,9 @@ int launch_rows(const RowsPlan& plan, void* stream);
 constexpr int kStagedDecline = -1;
 int launch_staged(const StagedPlan& plan, void* stream);
 int launch_update_rows(const UpdRowsPlan& plan, void* stream);
+// Launch trace (diagnostics): record every kernel instantiation launched from
+// here on (on: clears the record); traced_kernels writes "name count" lines.
+void trace_kernels(bool on);
+size_t traced_kernels(char* buf, size_t cap);
 
 }  // namespace xrs

@@ -199,6 +199,47 @@ def gather_seconds(elapsed: float, device=None) -> List[float]:
     return [float(v) for v in t.cpu()]
 
 
+class SharedDevice(RuntimeError):
+    """Two ranks resolved to the same GPU outside a labelled rehearsal."""
+
+
+def rehearsal_env(env=None) -> bool:
+    """XRS_REHEARSAL=1: ranks may share a card (one-GPU rehearsals of the
+    multi-rank path); the bench line then says "shared_gpu": true."""
+    env = os.environ if env is None else env
+    return env.get("XRS_REHEARSAL", "") not in ("", "0")
+
+
+def gather_objects(obj) -> list:
+    """Every rank's picklable `obj`, indexed by rank (over the process group;
+    [obj] without one)."""
+    if not _ddp():
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def check_distinct_devices(rank_devices: Sequence[dict], rehearsal: bool) -> bool:
+    """True when two ranks share a GPU (same "pci" address).  Outside a
+    rehearsal that is an error: a line claiming N GPUs must have run on N."""
+    seen = {}
+    shared = False
+    for d in rank_devices:
+        key = d["pci"]
+        if key in seen:
+            shared = True
+            if not rehearsal:
+                raise SharedDevice(
+                    f"ranks {seen[key]} and {d['rank']} run on the same GPU ({key}); one rank "
+                    f"per GPU is required (XRS_REHEARSAL=1 for a labelled one-card rehearsal)")
+        else:
+            seen[key] = d["rank"]
+    return shared
+
+
 def timed_steps(step: Callable[[int], None], steps: int, warmup: int, sync: Callable[[], None],
                 device=None) -> List[float]:
     """`warmup` untimed steps, then exactly `steps` steps bracketed by barrier +

@@ -224,7 +224,8 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     o.encode_batch(host, size, n)
     s = torch.cuda.current_stream().cuda_stream
     for lost, need in (([0, 1], [0, 1]), ([0, 1, 2], [0, 1, 2]), ([0, 1, 2, 3], [0, 1, 2, 3]),
-                       ([4, 9], [9, 4]), ([2, 5, 11], [5]), ([1, 13], [1, 13]), ([3, 7, 8], [])):
+                       ([4, 9], [9, 4]), ([2, 5, 11], [5]), ([1, 13], [1, 13]), ([3, 7, 8], []),
+                       ([12], [12]), ([14], [14])):
         h = host.copy()
         h[:, lost] = 0x5A
         has = [i for i in range(D + P) if i not in lost]

@@ -28,7 +28,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 \
+      python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 --ramp-seconds 0.5 \
       --xgmi-stripes 0 || exit $?
 fi
 exit 0

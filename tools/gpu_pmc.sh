@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 --xgmi-stripes 0"
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 --xgmi-stripes 0 --ramp-seconds 0.3 --no-parity"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- $B \
   > gpurun_out/pmc_fetch.log 2>&1 || { echo "fetch pass rc=$?"; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- $B \

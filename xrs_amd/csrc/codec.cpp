@@ -90,7 +90,11 @@ int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, boo
       plan.acc = acc || c0 > 0;
       // one launch covers the whole Encode: source c = data c, piggyback
       // target 1 + c % (p-1) (makeXORSet, xrs.go:77-100)
-      plan.encode_xs = encode && np <= xrs::kMaxOut && ns <= xrs::kMaxSrc;
+      plan.encode_xs = encode && np <= xrs::kMaxOut && ns <= xrs::kMaxSrc && np >= 2;
+      // ... and only with sources in makeXORSet order: the compile-time
+      // kernels hard-code that piggyback target and ignore plan.pb
+      for (int c = 0; c < C && plan.encode_xs; ++c)
+        plan.encode_xs = src[c0 + c].pb == 1 + c % (np - 1);
       plan.half = half;
       plan.n_stripes = n_stripes;
       for (int r = 0; r < P; ++r) plan.dst[r] = dst[g0 + r];
@@ -1014,11 +1018,16 @@ int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* s
   // 4-16 KiB vects 6-16% faster (12+3 @ 4 KiB 0.657 -> 0.752 of 8 TB/s, 10+4
   // +10%, 13+2 +16%) and Encode 0-5%; from 64 KiB up it moves both by
   // -1.3..+3.7% (tools/layout_ab.py, profiles/r02_layout_*.log).
+  // Callers size a batch as n_stripes * stripe_stride (which may exceed
+  // n_shards * shard_stride by up to 1/7).  Sizes whose strides would not fit
+  // in size_t are refused.
   const size_t pad = size >= (4u << 20) ? 4096 + 256 : 0;
+  if (size > SIZE_MAX / 2 / static_cast<size_t>(n_shards)) return XRS_ERR_INVALID_ARG;
   const size_t s = (size % 16 && size < (32u << 10)) ? size : (size + 15) / 16 * 16 + pad;
   const size_t packed = s * static_cast<size_t>(n_shards);
   size_t p2 = 1;
-  while (p2 < packed) p2 <<= 1;
+  while (p2 < packed && p2 <= SIZE_MAX / 2) p2 <<= 1;
+  if (p2 < packed) p2 = packed;  // no power of two above packed fits: keep it packed
   *shard_stride = s;
   *stripe_stride = (p2 - packed) * 7 <= packed ? p2 : packed;
   return XRS_OK;

@@ -1121,6 +1121,13 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
                                             : static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   }
   const dim3 g(static_cast<unsigned>(blocks));
+  if constexpr (NL == 1) {
+    // one lost parity vect (12+4: P12 -> nb = 15, P13..15 -> nb = 14)
+    if (p.nb == 15) {
+      XRS_LAUNCH((staged_ws_kernel<12, 15, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if (p.nb == 12)
     XRS_LAUNCH((staged_ws_kernel<12, 12, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   else if (p.nb == 13)
@@ -1326,6 +1333,20 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       }
       if (early) return launch_staged_ct_bs<NL, NN, kBlock, -1>(a, p, stream);
       return launch_staged_ct_bs<NL, NN, kBlock, 0>(a, p, stream);
+    }
+  }
+  if constexpr (VEC && NL == 1 && NN == 1) {
+    // One lost and needed parity vect of 12+4 (P12: nb = 15; P13-P15:
+    // nb = 14), every a-row a survivor: the compile-time wave-specialised
+    // kernel (reference bench xrs_test.go:523-574 patterns).
+    // XRS_STAGED_CT=0 keeps the runtime-count one below.
+    const char* cv = std::getenv("XRS_STAGED_CT");
+    const char* wv = std::getenv("XRS_STAGED_WS");
+    const bool ct1 = late && p.nd == 12 && p.na == 12 && p.nl == 1 && p.nn == 1 && p.nb >= 12 &&
+                     p.nb <= 15 && !(cv && cv[0] == '0') && !(wv && *wv);
+    if (ct1) {
+      if (p.half >= (256u << 10)) return launch_staged_ws<1, 1, 512>(a, p, stream);
+      return launch_staged_ws<1, 1, 256>(a, p, stream);
     }
   }
   if constexpr (VEC) {
@@ -1696,12 +1717,25 @@ int split_launch(Plan p, uint64_t len, bool aligned, F launch, bool overlap_ok =
 
 bool row_aligned(const RowRef& r) { return aligned16(r.ptr) && aligned16(r.stripe_stride); }
 
-// Two rows of `len` bytes (stripe 0) share a byte, or step differently
-// (then assume they may meet in some stripe).
-bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len) {
+// Two rows of `len` bytes share a byte in some pair of stripes s, t <
+// n_stripes (row a of stripe s against row b of stripe t), or step
+// differently (then assume they may meet).  With equal strides S the rows
+// meet iff |delta - m*S| < len for some m in (-n_stripes, n_stripes), delta =
+// b.ptr - a.ptr; the nearest m are floor(delta / S) and the next one, clamped.
+bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len, uint64_t n_stripes) {
   if (a.stripe_stride != b.stripe_stride) return true;
-  const uint64_t lo = a.ptr < b.ptr ? a.ptr : b.ptr, hi = a.ptr < b.ptr ? b.ptr : a.ptr;
-  return hi - lo < len;
+  const __int128 delta = static_cast<__int128>(b.ptr) - static_cast<__int128>(a.ptr);
+  const __int128 S = a.stripe_stride;
+  auto near = [&](__int128 m) {
+    const __int128 r = delta - m * S;
+    return (r < 0 ? -r : r) < static_cast<__int128>(len);
+  };
+  if (S == 0 || n_stripes <= 1) return near(0);
+  const __int128 hi = static_cast<__int128>(n_stripes) - 1, lo = -hi;
+  __int128 q = delta / S;
+  if (delta % S != 0 && delta < 0) --q;  // floor
+  const __int128 m0 = q < lo ? lo : (q > hi ? hi : q), m1 = q + 1 < lo ? lo : (q + 1 > hi ? hi : q + 1);
+  return near(m0) || near(m1);
 }
 
 }  // namespace
@@ -1736,7 +1770,7 @@ int launch_pair(const PairPlan& p0, void* stream) {
   pp.overlap = false;
   bool pure = !p0.acc;  // no accumulate, and no destination that is also a source
   for (int r = 0; r < p0.P && pure; ++r)
-    for (int c = 0; c < p0.C && pure; ++c) pure = !rows_overlap(p0.dst[r], p0.src[c], 2 * p0.half);
+    for (int c = 0; c < p0.C && pure; ++c) pure = !rows_overlap(p0.dst[r], p0.src[c], 2 * p0.half, p0.n_stripes);
   return split_launch(pp, p0.half, al, [s](const PairPlan& p, bool vec) {
     if (p.acc) return vec ? launch_pair_p<true, true>(p, s) : launch_pair_p<true, false>(p, s);
     return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
@@ -1792,8 +1826,8 @@ int launch_rows(const RowsPlan& p0, void* stream) {
   rp.overlap = false;
   bool pure = !p0.acc;  // no accumulate, and no destination that is also a source
   for (int r = 0; r < p0.R && pure; ++r) {
-    for (int m = 0; m < p0.NM && pure; ++m) pure = !rows_overlap(p0.dst[r], p0.msrc[m], p0.len);
-    for (int x = 0; x < p0.NX && pure; ++x) pure = !rows_overlap(p0.dst[r], p0.xsrc[x], p0.len);
+    for (int m = 0; m < p0.NM && pure; ++m) pure = !rows_overlap(p0.dst[r], p0.msrc[m], p0.len, p0.n_stripes);
+    for (int x = 0; x < p0.NX && pure; ++x) pure = !rows_overlap(p0.dst[r], p0.xsrc[x], p0.len, p0.n_stripes);
   }
   return split_launch(rp, p0.len, al, [s](const RowsPlan& p, bool vec) {
     if (p.acc) return vec ? launch_rows_r<true, true>(p, s) : launch_rows_r<true, false>(p, s);

@@ -105,6 +105,15 @@ int xrs_replace(const xrs_codec *codec, uint8_t *const *data, const int *rows, i
  * costs at most 1/7 more).  Any layout works; this one streams fastest on
  * MI355X. */
 int xrs_batch_strides(size_t size, int n_shards, size_t *shard_stride, size_t *stripe_stride);
+/* xrs_batch_strides plus a base offset (0..15 bytes): place the batch at
+ * (16-B-aligned allocation) + base_offset, so that the b-half of every shard
+ * (vect[S/2:]) is aligned when S/2 is not a multiple of 16 (odd vect sizes:
+ * 0 for sizes that are multiples of 32).  A batch of n stripes needs
+ * base_offset + n * stripe_stride bytes (stripe_stride may exceed
+ * n_shards * shard_stride).  Any layout is correct; this one streams fastest
+ * ("Any size, any alignment"). */
+int xrs_batch_layout(size_t size, int n_shards, size_t *shard_stride, size_t *stripe_stride,
+                     size_t *base_offset);
 /* Encode n_stripes stripes in place.  One fused pass: RS + piggyback. */
 int xrs_encode_batched(const xrs_codec *codec, uint8_t *base, size_t size,
                        size_t shard_stride, size_t stripe_stride, size_t n_stripes,

@@ -148,6 +148,26 @@ def test_single_hip_runtime():
     assert r.returncode == 0, r.stderr[-2000:]
 
 
+def test_batch_layout_offset():
+    """xrs_batch_layout: the strides of xrs_batch_strides and the base offset
+    that puts shard 0's b-half (vect[S/2:]) on 16 B: 0 for sizes that are
+    multiples of 32 (profiles/r03_layout_odd.log)."""
+    for size in (2, 4, 34, 1026, 4096, 4098, 4100, 4126, 65538, 1 << 20, (1 << 20) + 2, 8 << 20):
+        sh, st, off = xrs_amd.batch_layout(size, 16)
+        assert (sh, st) == xrs_amd.batch_strides(size, 16)
+        assert 0 <= off < 16 and (off + size // 2) % 16 == 0, size
+    assert xrs_amd.batch_layout(4096, 16)[2] == 0 and xrs_amd.batch_layout(4100, 16)[2] == 14
+    assert xrs_amd.batch_layout((1 << 20) + 2, 16)[2] == 15
+    with pytest.raises(xrs_amd.XRSError):
+        xrs_amd.batch_layout(4096, 0)
+    # strides that would not fit in size_t are refused (no wrap-around)
+    for size in (1 << 62, (1 << 64) - 2):
+        with pytest.raises(xrs_amd.XRSError):
+            xrs_amd.batch_strides(size, 16)
+    sh, st = xrs_amd.batch_strides(1 << 58, 16)
+    assert sh == (1 << 58) + 4352 and st >= 16 * sh
+
+
 def test_batch_strides_recommendation():
     """xrs_batch_strides (codec.cpp): shards back to back below 4 MiB, odd
     sizes back to back below 32 KiB, 16-rounded from there, a 4 KiB + 256 B

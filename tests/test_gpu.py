@@ -628,36 +628,40 @@ def test_replace_batched_every_n_vs_oracle(cuda, rng, monkeypatch, mode, size, n
         assert np.array_equal(tp.cpu().numpy(), ref), (nrep, rows)
 
 
-@pytest.mark.parametrize("d,p,size", [(12, 3, 4096), (10, 4, 4096), (13, 2, 4100), (12, 3, 1 << 16),
-                                      (12, 4, 4096)])
-def test_recommended_layout_vs_oracle(cuda, rng, d, p, size):
-    """The layout xrs_batch_strides recommends (a power-of-two stripe stride
-    with a gap after the last shard when that costs <= 1/7, codec.cpp):
-    Encode, every ReconstOne and a 2-loss Reconst against the oracle, with
-    the gap bytes untouched."""
-    shard, stripe = xrs_amd.batch_strides(size, d + p)
-    n = 24
-    buf = rng.integers(0, 256, size=n * stripe, dtype=np.uint8)
+@pytest.mark.parametrize("d,p,size,n", [(12, 3, 4096, 24), (10, 4, 4096, 24), (13, 2, 4100, 24),
+                                        (12, 3, 1 << 16, 24), (12, 4, 4096, 24), (12, 4, 4100, 600),
+                                        (12, 4, 4098, 600), (12, 4, 1048578, 6)])
+def test_recommended_layout_vs_oracle(cuda, rng, d, p, size, n):
+    """The layout xrs_batch_layout recommends (a power-of-two stripe stride
+    with a gap after the last shard when that costs <= 1/7; odd sizes shifted
+    by the base offset that aligns the b-halves, codec.cpp): Encode, every
+    ReconstOne and a 2-loss Reconst against the oracle, full-chip grids for
+    the odd 12+4 sizes, with the gap and offset bytes untouched."""
+    shard, stripe, off = xrs_amd.batch_layout(size, d + p)
+    assert (shard, stripe) == xrs_amd.batch_strides(size, d + p)
+    assert off == (16 - (size // 2) % 16) % 16
+    buf = rng.integers(0, 256, size=off + n * stripe, dtype=np.uint8)
     x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
 
     def rows(b, s):
-        return [b[s * stripe + i * shard:][:size] for i in range(d + p)]
+        return [b[off + s * stripe + i * shard:][:size] for i in range(d + p)]
 
     ref = buf.copy()
     for s in range(n):
         v = [r.copy() for r in rows(ref, s)]
         o.encode(v)
         for i in range(d + p):
-            ref[s * stripe + i * shard:][:size] = v[i]
+            ref[off + s * stripe + i * shard:][:size] = v[i]
     t = to_dev(buf, cuda)
-    x.encode_batched(t.data_ptr(), size, shard, stripe, n, stream())
+    base = t.data_ptr() + off
+    x.encode_batched(base, size, shard, stripe, n, stream())
     torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), ref)  # gaps included
     for k in range(d):
         t = to_dev(ref, cuda)
-        for s in range(n):
-            t[s * stripe + k * shard:s * stripe + k * shard + size] = 0x5A
-        x.reconst_one_batched(t.data_ptr(), size, shard, stripe, n, k, stream())
+        tv = t[off:off + n * stripe].view(n, stripe)
+        tv[:, k * shard:k * shard + size] = 0x5A
+        x.reconst_one_batched(t.data_ptr() + off, size, shard, stripe, n, k, stream())
         torch.cuda.synchronize()
         assert np.array_equal(t.cpu().numpy(), ref), k
     lost = [0, d - 1]
@@ -669,11 +673,11 @@ def test_recommended_layout_vs_oracle(cuda, rng, d, p, size):
             v[i][:] = 0
         o.reconst(v, has, lost)
         for i in range(d + p):
-            exp[s * stripe + i * shard:][:size] = v[i]
+            exp[off + s * stripe + i * shard:][:size] = v[i]
     t = to_dev(ref, cuda)
-    for s in range(n):
-        for i in lost:
-            t[s * stripe + i * shard:s * stripe + i * shard + size] = 0
-    x.reconst_batched(t.data_ptr(), size, shard, stripe, n, has, lost, stream())
+    tv = t[off:off + n * stripe].view(n, stripe)
+    for i in lost:
+        tv[:, i * shard:i * shard + size] = 0
+    x.reconst_batched(t.data_ptr() + off, size, shard, stripe, n, has, lost, stream())
     torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), exp)

@@ -14,6 +14,9 @@
 //           (a one-dword spill load where the next lane is not contiguous),
 //           v_alignbyte by the 0..3-byte remainder
 //   mode 3  mode 2 for loads, temporal
+//   mode 4  mode 0 with floor(H/16) lanes per stripe: no wave straddles a
+//           stripe's ragged end; the last lane of each stripe also does the
+//           overlapping tail chunk
 // Not part of the product.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/oddrec_probe.hip -o tools/oddrec_probe
@@ -88,17 +91,31 @@ struct Rows {
 };
 
 template <int MODE>
+__device__ __forceinline__ void rec_body(const Rows& r, uint64_t base, uint32_t t0, uint32_t t1);
+
+template <int MODE>
 __global__ __launch_bounds__(256) void rec_mix(const Rows r, uint64_t stride, uint64_t len,
                                               uint64_t chunks, uint64_t total, uint32_t t0,
                                               uint32_t t1) {
-  constexpr bool NT = MODE == 0 || MODE == 2;
-  constexpr bool AL4 = MODE >= 2;
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (gid >= total) return;
   const uint64_t st = gid / chunks;
   uint64_t off = (gid - st * chunks) * 16;
+  if constexpr (MODE == 4) {
+    // floor(len/16) lanes per stripe (no lane straddles the ragged end); the
+    // last lane of each stripe also does the overlapping tail chunk
+    rec_body<0>(r, st * stride + off, t0, t1);
+    if (off + 16 == chunks * 16 && len % 16) rec_body<0>(r, st * stride + len - 16, t0, t1);
+    return;
+  }
   if (off > len - 16) off = len - 16;
-  const uint64_t base = st * stride + off;
+  rec_body<MODE>(r, st * stride + off, t0, t1);
+}
+
+template <int MODE>
+__device__ __forceinline__ void rec_body(const Rows& r, uint64_t base, uint32_t t0, uint32_t t1) {
+  constexpr bool NT = MODE == 0 || MODE == 2;
+  constexpr bool AL4 = MODE == 2 || MODE == 3;
   u32x4 x[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) x[m] = AL4 ? ld_al4<NT>(r.src[m] + base) : ld16<NT>(r.src[m] + base);
@@ -140,7 +157,7 @@ __global__ void al4_copy(uint64_t src, uint64_t dst, uint64_t n, uint64_t len, u
 
 template <int MODE>
 double run(const Rows& r, uint64_t stride, uint64_t len, uint64_t n) {
-  const uint64_t chunks = (len + 15) / 16, total = chunks * n;
+  const uint64_t chunks = MODE == 4 ? len / 16 : (len + 15) / 16, total = chunks * n;
   const uint32_t nblk = static_cast<uint32_t>((total + 255) / 256);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -204,9 +221,9 @@ int main(int argc, char** argv) {
       r.dst[0] = b + len;
       r.dst[1] = b;
       const double g0 = run<0>(r, stride, len, n), g1 = run<1>(r, stride, len, n);
-      const double g2 = run<2>(r, stride, len, n), g3 = run<3>(r, stride, len, n);
+      const double g2 = run<2>(r, stride, len, n), g4 = run<4>(r, stride, len, n);
       std::printf("{\"round\": %d, \"vect\": %d, \"gbs_direct_nt\": %.1f, \"gbs_direct_t\": %.1f, "
-                  "\"gbs_al4_nt\": %.1f, \"gbs_al4_t\": %.1f}\n", rep, S, g0, g1, g2, g3);
+                  "\"gbs_al4_nt\": %.1f, \"gbs_tail_lane\": %.1f}\n", rep, S, g0, g1, g2, g4);
       std::fflush(stdout);
     }
   CK(hipFree(buf));

@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
   }
   const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
   // --- plain sync calls, one thread
-  {
+  if (!(argc > 2 && std::strcmp(argv[2], "queue") == 0)) {
     std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, 1));
     std::vector<uint8_t*> p;
     for (auto& x : v) p.push_back(x.data());
@@ -123,10 +123,18 @@ int main(int argc, char** argv) {
     std::_Exit(0);
   }
   // --- batching queue, T threads
-  for (int upd = 0; upd < 2; ++upd)
-  for (int threads : {1, 8, 32, 128}) {
+  // `sync_bench SIZE queue [WAIT_US] [THREADS...]`: the queue only
+  const bool qonly = argc > 2 && std::strcmp(argv[2], "queue") == 0;
+  const int wait_us = qonly && argc > 3 ? std::atoi(argv[3]) : 50;
+  std::vector<int> tlist = {1, 8, 32, 128};
+  if (qonly && argc > 4) {
+    tlist.clear();
+    for (int i = 4; i < argc; ++i) tlist.push_back(std::atoi(argv[i]));
+  }
+  for (int upd = 0; upd < (qonly ? 1 : 2); ++upd)
+  for (int threads : tlist) {
     xrs_queue* q = nullptr;
-    if (xrs_queue_new(c, size, 1024, 50, &q)) return 4;
+    if (xrs_queue_new(c, size, 1024, wait_us, &q)) return 4;
     std::atomic<long> total{0};
     std::atomic<bool> stop{false};
     std::vector<std::thread> th;

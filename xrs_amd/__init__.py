@@ -17,7 +17,8 @@ import ctypes
 import os
 import threading
 
-__all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "hip_runtimes",
+__all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "batch_layout",
+           "hip_runtimes",
            "trace_kernels", "traced_kernels"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +88,7 @@ def _load():
         "xrs_update": ([P, P, P, Z, I, PP, I], I),
         "xrs_replace": ([P, PP, IP, I, Z, PP, I], I),
         "xrs_batch_strides": ([Z, I, ctypes.POINTER(Z), ctypes.POINTER(Z)], I),
+        "xrs_batch_layout": ([Z, I, ctypes.POINTER(Z), ctypes.POINTER(Z), ctypes.POINTER(Z)], I),
         "xrs_encode_batched": ([P, P, Z, Z, Z, Z, P], I),
         "xrs_reconst_one_batched": ([P, P, Z, Z, Z, Z, I, P], I),
         "xrs_reconst_batched": ([P, P, Z, Z, Z, Z, IP, I, IP, I, P], I),
@@ -189,6 +191,15 @@ def batch_strides(size: int, n_shards: int):
     a, b = ctypes.c_size_t(), ctypes.c_size_t()
     _raise(_lib.xrs_batch_strides(size, n_shards, ctypes.byref(a), ctypes.byref(b)))
     return a.value, b.value
+
+
+def batch_layout(size: int, n_shards: int):
+    """Recommended (shard_stride, stripe_stride, base_offset) for a device
+    batch: place it at a 16-B-aligned address + base_offset (odd vect sizes
+    get their b-halves aligned; xrs_batch_layout)."""
+    a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    _raise(_lib.xrs_batch_layout(size, n_shards, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return a.value, b.value, c.value
 
 
 def trace_kernels(on: bool = True) -> None:

@@ -1033,6 +1033,24 @@ int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* s
   return XRS_OK;
 }
 
+int xrs_batch_layout(size_t size, int n_shards, size_t* shard_stride, size_t* stripe_stride,
+                     size_t* base_offset) {
+  if (!base_offset) return XRS_ERR_INVALID_ARG;
+  const int e = xrs_batch_strides(size, n_shards, shard_stride, stripe_stride);
+  if (e) return e;
+  // An odd half (a vect size that is not a multiple of 32) leaves every
+  // b-half (vect[S/2:]) off 16-B alignment when the a-halves are aligned.
+  // ReconstOne reads 13 b-halves and 3 a-halves of 12+4, so the batch is
+  // shifted to put shard 0's b-half on a 16-B boundary: with the recommended
+  // strides every b-half is then 4-B (4,100, 4,098 B) or 16-B (1 MiB + 2)
+  // aligned.  Measured on MI355X (tools/layout_ab.py,
+  // profiles/r03_layout_odd.log, fraction of 8 TB/s): ReconstOne 4,100 B
+  // 0.602 -> 0.684, 4,098 B 0.594 -> 0.663, 1 MiB + 2 0.643 -> 0.716;
+  // 2-lost Reconst +2..+8%; Encode unchanged (reads a- and b-halves alike).
+  *base_offset = (16 - (size / 2) % 16) % 16;
+  return XRS_OK;
+}
+
 int xrs_encode_batched(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
                        size_t stripe_stride, size_t n_stripes, void* stream) {
   if (!x) return XRS_ERR_INVALID_ARG;

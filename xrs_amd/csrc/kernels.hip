@@ -75,10 +75,17 @@ __device__ __forceinline__ uint32_t gmul(const GfTab& t, const Sel& s) {
 // every shard byte is touched exactly once per launch (measured on MI355X:
 // nt loads + nt stores +3% Encode, +7..11% ReconstOne; tools/kbench.hip).
 // !VEC: nb (1..4) single-byte accesses (any alignment, ragged tail).
+#ifndef XRS_LOAD_NT
+#define XRS_LOAD_NT 1  // -DXRS_LOAD_NT=0: temporal 16-byte loads (A/B builds only)
+#endif
 template <bool VEC>
 __device__ __forceinline__ void ld(uint32_t* v, uint64_t addr, int nb) {
   if constexpr (VEC) {
+#if XRS_LOAD_NT
     const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(addr));
+#else
+    const u32x4 t = *reinterpret_cast<const gu32x4*>(addr);
+#endif
     v[0] = t.x;
     v[1] = t.y;
     v[2] = t.z;

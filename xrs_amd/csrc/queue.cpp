@@ -90,6 +90,7 @@ struct xrs_queue {
   std::condition_variable cv_work, cv_free;
   std::thread worker[kMaxWorkers];
   int n_workers = 2, n_batches = 4;
+  bool eager = false;  // XRS_QUEUE_POLICY=free: a free worker runs the open batch at once
 
   // One copy between a caller's buffer and its staged stripe: `len` bytes at
   // staging row `row` (row * size + off) <-> host + off.
@@ -170,6 +171,15 @@ void xrs_queue::work() {
       Batch& bt = b[i];
       if (bt.state == OPEN || bt.state == CLOSED) pending = true;
       if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
+      if (eager && bt.state == OPEN && bt.reserved > 0) {
+        // A free worker closes the open batch at once: later callers start
+        // the next batch, and this one runs when its reserved stripes are
+        // staged (the last filler wakes a worker).
+        bt.state = CLOSED;
+        if (open == i) open = -1;
+        if (bt.filled == bt.reserved) pick = i;
+        continue;
+      }
       if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
         // A small batch runs at once when no batch is in flight (a lone
         // caller does not wait for company); otherwise, and for large
@@ -178,7 +188,7 @@ void xrs_queue::work() {
         const auto due = bt.opened + max_wait;
         const bool small = bt.reserved * stripe_bytes <= zc_max;
         // (stopping: drain, every caller already in gets its result)
-        if ((running == 0 && small) || stop || Clock::now() >= due) {
+        if ((running == 0 && small) || eager || stop || Clock::now() >= due) {
           bt.state = CLOSED;
           if (open == i) open = -1;
           pick = i;
@@ -316,6 +326,8 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   const char* wv = std::getenv("XRS_QUEUE_WORKERS");
   if (wv && *wv) q->n_workers = std::max(1, std::min(kMaxWorkers, std::atoi(wv)));
   q->n_batches = q->n_workers + 2;
+  const char* pv = std::getenv("XRS_QUEUE_POLICY");
+  q->eager = pv && std::strcmp(pv, "free") == 0;
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);

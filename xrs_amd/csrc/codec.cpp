@@ -1029,7 +1029,7 @@ int xrs_batch_strides(size_t size, int n_shards, size_t* shard_stride, size_t* s
   while (p2 < packed && p2 <= SIZE_MAX / 2) p2 <<= 1;
   if (p2 < packed) p2 = packed;  // no power of two above packed fits: keep it packed
   *shard_stride = s;
-  *stripe_stride = (p2 - packed) * 7 <= packed ? p2 : packed;
+  *stripe_stride = (p2 - packed) <= packed / 7 ? p2 : packed;
   return XRS_OK;
 }
 

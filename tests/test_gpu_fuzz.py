@@ -43,7 +43,7 @@ def draw_case(rng):
         n = -(-65536 * 32 // size) + int(rng.integers(0, 64))  # >= 65,536 16-byte lanes
     shard = size + int(rng.choice([0, 0, 2, 16, 256]))
     stripe = (d + p) * shard + int(rng.choice([0, 0, 6, 64]))
-    base = int(rng.choice([0, 0, 0, 1, 8]))
+    base = int(rng.choice([0, 0, 0, 1, 8, 14, 15]))  # 14, 15: xrs_batch_layout offsets
     return d, p, size, n, shard, stripe, base, OPS[int(rng.integers(0, len(OPS)))]
 
 

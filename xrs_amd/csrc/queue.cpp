@@ -171,15 +171,6 @@ void xrs_queue::work() {
       Batch& bt = b[i];
       if (bt.state == OPEN || bt.state == CLOSED) pending = true;
       if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
-      if (eager && bt.state == OPEN && bt.reserved > 0) {
-        // A free worker closes the open batch at once: later callers start
-        // the next batch, and this one runs when its reserved stripes are
-        // staged (the last filler wakes a worker).
-        bt.state = CLOSED;
-        if (open == i) open = -1;
-        if (bt.filled == bt.reserved) pick = i;
-        continue;
-      }
       if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
         // A small batch runs at once when no batch is in flight (a lone
         // caller does not wait for company); otherwise, and for large

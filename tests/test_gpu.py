@@ -603,6 +603,41 @@ def test_compile_time_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, 
             assert np.array_equal(t.cpu().numpy(), ref), (size, k)
 
 
+PAD_CODECS = [(11, 4), (13, 4), (9, 3), (7, 3), (18, 4), (5, 4), (15, 4), (9, 2)]
+
+
+@pytest.mark.parametrize("mode", ["pad", "nopad"])
+@pytest.mark.parametrize("d,p", PAD_CODECS)
+def test_padded_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, p):
+    """Codecs without their own compile-time Encode / ReconstOne shape run
+    the nearest larger instantiation with up to 3 padding rows (zero tables,
+    no piggyback; kernels.hip pad_count); XRS_PAD=0 runs the runtime-count
+    kernels.  Both against the oracle on full grids and ragged sizes, every
+    k, and the trace names the padded instantiation."""
+    if mode == "nopad":
+        monkeypatch.setenv("XRS_PAD", "0")
+    x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+    for size, n in ((4096, 520), (4100, 33), (1 << 20, 2)):
+        host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)
+        t = to_dev(host, cuda)
+        xrs_amd.trace_kernels(True)
+        x.encode_batched(t.data_ptr(), size, size, (d + p) * size, n, stream())
+        torch.cuda.synchronize()
+        xrs_amd.trace_kernels(False)
+        names = list(xrs_amd.traced_kernels())
+        if size == 4096:  # compile-time counts (pair_kernel<p, C, ...>) vs runtime (-1)
+            assert (f"pair_kernel<{p}, -1," in names[0]) == (mode == "nopad"), names
+        ref = host.copy()
+        o.encode_batch(ref, size, n)
+        assert np.array_equal(t.cpu().numpy(), ref), size
+        for k in range(d):
+            t = to_dev(ref, cuda)
+            t[:, k] = 0x5A
+            x.reconst_one_batched(t.data_ptr(), size, size, (d + p) * size, n, k, stream())
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), ref), (size, k)
+
+
 @pytest.mark.parametrize("mode", ["ct", "dyn"])
 @pytest.mark.parametrize("size,n", [(4096, 40), (9000, 20), (8200, 9), (34, 30)])
 def test_replace_batched_every_n_vs_oracle(cuda, rng, monkeypatch, mode, size, n):

@@ -274,8 +274,9 @@ __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
       // launched for a whole Encode (PairPlan::encode_xs).
 #pragma unroll
       for (int c = 0; c < C; ++c)
+        if (c < a.n_src)  // (wave-uniform: padding sources past n_src ride on nothing)
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+          for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
     } else {
 #pragma unroll
       for (int c = 0; c < C; ++c) piggyback<P, W>(acc_b, a.pbmask, c, xa[c]);
@@ -1454,7 +1455,7 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   }
   for (int c = 0; c < n; ++c)
     if (p.pb[c] >= 0) a.pbmask[p.pb[c]] |= 1u << c;
-  a.n_src = n;
+  a.n_src = p.npb > 0 ? p.npb : n;
   a.half = p.half;
   a.off0 = p.off0;
   a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
@@ -1536,6 +1537,25 @@ int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int
   return rc;
 }
 
+// Padding to a compile-time shape: a source count without its own
+// instantiation runs the smallest instantiated count above it when that adds
+// at most kPadRows rows.  Padding rows repeat row 0's address (their loads
+// hit the cache lines row 0 just brought in) with zero tables, and ride on
+// no parity (PairArgs::n_src / RowsArgs xmask 0), so the result is the same.
+constexpr int kPadRows = 3;
+
+template <int... Cs>
+int pad_count(int c, std::integer_sequence<int, Cs...>) {
+  int best = -1;
+  (void)((Cs > c && Cs <= c + kPadRows && (best < 0 || Cs < best) && (best = Cs, true)) || ...);
+  return best;
+}
+
+bool pad_disabled() {
+  const char* e = std::getenv("XRS_PAD");
+  return e && e[0] == '0';
+}
+
 // Compile-time source counts of an accumulating launch with four outputs:
 // Replace(n) at p = 4, n = 1..8 (the reference's Replace benchmark,
 // xrs_test.go:627-680).
@@ -1552,6 +1572,19 @@ int launch_pair_c(const PairPlan& p, hipStream_t s) {
     if (p.encode_xs && !std::getenv("XRS_ENCODE_DYN")) {
       const int rc = launch_encode_ct<P, VEC>(p, s, typename EncodeShapes<P>::type{});
       if (rc != -1) return rc;
+      const int cs = pad_count(p.C, typename EncodeShapes<P>::type{});
+      if (cs > 0 && p.C > 0 && !pad_disabled()) {
+        PairPlan q = p;
+        for (int c = p.C; c < cs; ++c) {
+          q.src[c] = p.src[0];
+          for (int r = 0; r < kMaxOut; ++r) q.tab[c][r] = GfTab{0, 0, 0, 0, 0};
+          q.pb[c] = -1;
+        }
+        q.npb = p.C;
+        q.C = cs;
+        const int prc = launch_encode_ct<P, VEC>(q, s, typename EncodeShapes<P>::type{});
+        if (prc != -1) return prc;
+      }
     }
   }
   if constexpr (ACC && VEC && P == 4) {
@@ -1651,17 +1684,49 @@ int launch_rows_c(const RowsPlan& p, hipStream_t s) {
     // profiles/r02_others_ab.log).
     const bool fits = p.len < (256u << 10) || p.NM + p.NX <= 22;
     if (fits && !std::getenv("XRS_ROWS_DYN")) {
-      const int rc = launch_reconst_one_ct<VEC>(
-          p, s, Shape2<12, 4>{},                     // 12+4
-          Shape2<4, 4>{}, Shape2<6, 3>{},            // 4+2, 6+3
-          Shape2<8, 2>{}, Shape2<8, 3>{},            // 8+4
-          Shape2<10, 3>{}, Shape2<10, 4>{},          // 10+4
-          Shape2<12, 6>{},                           // 12+3
-          Shape2<14, 4>{}, Shape2<14, 5>{},          // 14+4
-          Shape2<16, 5>{}, Shape2<16, 6>{},          // 16+4
-          Shape2<20, 6>{}, Shape2<20, 7>{},          // 20+4
-          Shape2<10, 10>{});                         // 10+2
+      auto ct = [&](const RowsPlan& q) {
+        return launch_reconst_one_ct<VEC>(
+            q, s, Shape2<12, 4>{},                     // 12+4
+            Shape2<4, 4>{}, Shape2<6, 3>{},            // 4+2, 6+3
+            Shape2<8, 2>{}, Shape2<8, 3>{},            // 8+4
+            Shape2<10, 3>{}, Shape2<10, 4>{},          // 10+4
+            Shape2<12, 6>{},                           // 12+3
+            Shape2<14, 4>{}, Shape2<14, 5>{},          // 14+4
+            Shape2<16, 5>{}, Shape2<16, 6>{},          // 16+4
+            Shape2<20, 6>{}, Shape2<20, 7>{},          // 20+4
+            Shape2<10, 10>{});                         // 10+2
+      };
+      const int rc = ct(p);
       if (rc != -1) return rc;
+      // Pad to the nearest instantiated (NM, NX) with at most kPadRows rows
+      // added in all (a codec without its own ReconstOne shape: 11+4, 13+4,
+      // 9+3, ...): padding GF rows repeat msrc[0] with zero tables, padding
+      // XOR rows repeat xsrc[0] (or msrc[0]) with mask 0.
+      static constexpr int kShapes[][2] = {{12, 4}, {4, 4}, {6, 3}, {8, 2}, {8, 3}, {10, 3},
+                                           {10, 4}, {12, 6}, {14, 4}, {14, 5}, {16, 5},
+                                           {16, 6}, {20, 6}, {20, 7}, {10, 10}};
+      int bm = -1, bx = -1;
+      for (const auto& sh : kShapes) {
+        const int add = (sh[0] - p.NM) + (sh[1] - p.NX);
+        if (sh[0] < p.NM || sh[1] < p.NX || add == 0 || add > kPadRows) continue;
+        if (p.len >= (256u << 10) && sh[0] + sh[1] > 22) continue;
+        if (bm < 0 || add < (bm - p.NM) + (bx - p.NX)) bm = sh[0], bx = sh[1];
+      }
+      if (bm > 0 && p.NM > 0 && !pad_disabled()) {
+        RowsPlan q = p;
+        for (int m = p.NM; m < bm; ++m) {
+          q.msrc[m] = p.msrc[0];
+          for (int r = 0; r < kMaxOut; ++r) q.tab[m][r] = GfTab{0, 0, 0, 0, 0};
+        }
+        for (int x = p.NX; x < bx; ++x) {
+          q.xsrc[x] = p.NX > 0 ? p.xsrc[0] : p.msrc[0];
+          q.xmask[x] = 0;
+        }
+        q.NM = bm;
+        q.NX = bx;
+        const int prc = ct(q);
+        if (prc != -1) return prc;
+      }
     }
   }
   return launch_rows_t<R, kDyn, kDyn, ACC, VEC>(p, s);

@@ -1,0 +1,79 @@
+"""Register and scratch budgets of the gfx950 kernels, read from the code
+object inside xrs_amd/libxrs_hip.so (no GPU needed): the AMDGPU metadata
+notes give each kernel's VGPR / AGPR count and private (scratch) segment.
+
+A bandwidth kernel here holds every row it reads in registers, so its wave
+occupancy is set by its VGPR count; a source change that pushes the headline
+Encode from 170 VGPRs past 256 (AGPRs in use, one wave per SIMD) cost 26-43%
+on the padded shapes before it was caught (profiles/r03_pad_ab.log).  These
+budgets pin the headline instantiations and the staged Reconst kernels."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "xrs_amd", "libxrs_hip.so")
+LLVM = "/opt/rocm/llvm/bin"
+
+# (symbol regex, max VGPRs) -- the kernels bench.py and smoke() run
+BUDGETS = [
+    (r"pair_kernelILi4ELi12ELb0ELb1ELi128ELb1E", 176),   # Encode 12+4 @ 1 MiB (dominant)
+    (r"pair_kernelILi4ELi12ELb0ELb1ELi128ELb0E", 176),   # Encode 12+4 @ 4 KiB
+    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi1024E", 128),  # ReconstOne @ 1 MiB (1024-thread blocks)
+    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi256E", 128),   # ReconstOne @ 4 KiB
+    (r"staged_ws_kernelILi12ELi14ELi2ELi2ELi256ELi1E", 128),
+    (r"staged_ws_kernelILi12ELi15ELi1ELi1ELi256ELi1E", 128),
+]
+
+
+def _notes(tmp_path):
+    for tool in ("objcopy",):
+        if not shutil.which(tool):
+            pytest.skip(f"{tool} not available")
+    if not os.path.exists(os.path.join(LLVM, "llvm-readelf")):
+        pytest.skip("ROCm LLVM tools not available")
+    fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB], check=True)
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
+                    f"--output={co}", "--unbundle"], check=True)
+    return subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
+                          capture_output=True, text=True, check=True).stdout
+
+
+def _kernels(txt):
+    starts = [m.start() for m in re.finditer(r"\.agpr_count:", txt)] + [len(txt)]
+    out = {}
+    for a, b in zip(starts, starts[1:]):
+        blk = txt[a:b]
+
+        def field(k):
+            m = re.search(r"\.%s:\s+(\S+)" % k, blk)
+            return m.group(1) if m else None
+        sym = field("symbol")
+        if sym:
+            out[sym] = {"vgpr": int(field("vgpr_count")), "agpr": int(field("agpr_count")),
+                        "scratch": int(field("private_segment_fixed_size"))}
+    return out
+
+
+def test_kernel_register_budgets(tmp_path):
+    ks = _kernels(_notes(tmp_path))
+    assert len(ks) > 100  # every instantiation is in the code object
+    for pat, vmax in BUDGETS:
+        hits = {s: v for s, v in ks.items() if re.search(pat, s)}
+        assert hits, pat
+        for s, v in hits.items():
+            assert v["agpr"] == 0 and v["vgpr"] <= vmax, (s, v)
+    # No kernel a default dispatch can launch spills to scratch.  The two
+    # that do are A/B-only: the 5-wave-capped staged kernel (T = 128, OCC =
+    # 5: XRS_STAGED_WS=128o5) and 1024-thread ReconstOne blocks for 20+4
+    # (26-27 rows; the launcher takes 1024-thread blocks only up to 22 rows,
+    # XRS_ROWS_BLOCK=1024 forces them).
+    ab_only = re.compile(r"staged_ws_kernelILi12ELi1[234]ELi[34]ELi[34]ELi128ELi5E|"
+                         r"rows_kernelILi2ELi20ELi[67]ELb0ELb1ELi1024E")
+    spills = {s: v for s, v in ks.items() if v["scratch"] and not ab_only.search(s)}
+    assert not spills, list(spills)[:5]

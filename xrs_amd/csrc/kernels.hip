@@ -274,9 +274,8 @@ __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
       // launched for a whole Encode (PairPlan::encode_xs).
 #pragma unroll
       for (int c = 0; c < C; ++c)
-        if (c < a.n_src)  // (wave-uniform: padding sources past n_src ride on nothing)
 #pragma unroll
-          for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
+        for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
     } else {
 #pragma unroll
       for (int c = 0; c < C; ++c) piggyback<P, W>(acc_b, a.pbmask, c, xa[c]);
@@ -1455,7 +1454,7 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   }
   for (int c = 0; c < n; ++c)
     if (p.pb[c] >= 0) a.pbmask[p.pb[c]] |= 1u << c;
-  a.n_src = p.npb > 0 ? p.npb : n;
+  a.n_src = n;
   a.half = p.half;
   a.off0 = p.off0;
   a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
@@ -1537,12 +1536,35 @@ int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int
   return rc;
 }
 
-// Padding to a compile-time shape: a source count without its own
+// Padding to a compile-time Encode shape: a source count without its own
 // instantiation runs the smallest instantiated count above it when that adds
-// at most kPadRows rows.  Padding rows repeat row 0's address (their loads
-// hit the cache lines row 0 just brought in) with zero tables, and ride on
-// no parity (PairArgs::n_src / RowsArgs xmask 0), so the result is the same.
+// at most kPadRows rows.  A padding row is an all-zero row (zero_rows(), read
+// with stripe stride 0, so every stripe reads the same few cache lines): its
+// GF products and its piggyback XOR are zero, and the kernel is unchanged (a
+// guard on the piggyback instead raised the 12+4 Encode from 170 to 258
+// VGPRs).
 constexpr int kPadRows = 3;
+constexpr uint64_t kZeroRowBytes = 16u << 20;  // vects up to 16 MiB pad; larger run the runtime kernel
+
+// Device address of kZeroRowBytes zero bytes on the current device (made
+// once per device, never freed: a launch in flight may read it), or 0.
+uint64_t zero_rows() {
+  static std::mutex mu;
+  static uint64_t buf[64] = {};
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (!buf[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, kZeroRowBytes) != hipSuccess) return 0;
+    if (hipMemset(p, 0, kZeroRowBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return 0;
+    }
+    buf[dev] = reinterpret_cast<uint64_t>(p);
+  }
+  return buf[dev];
+}
 
 template <int... Cs>
 int pad_count(int c, std::integer_sequence<int, Cs...>) {
@@ -1573,15 +1595,17 @@ int launch_pair_c(const PairPlan& p, hipStream_t s) {
       const int rc = launch_encode_ct<P, VEC>(p, s, typename EncodeShapes<P>::type{});
       if (rc != -1) return rc;
       const int cs = pad_count(p.C, typename EncodeShapes<P>::type{});
-      if (cs > 0 && p.C > 0 && !pad_disabled()) {
+      const uint64_t z = (cs > 0 && p.C > 0 && 2 * p.half <= kZeroRowBytes && !pad_disabled())
+                             ? zero_rows() : 0;
+      if (z) {
         PairPlan q = p;
         for (int c = p.C; c < cs; ++c) {
-          q.src[c] = p.src[0];
+          q.src[c] = RowRef{z, 0};
           for (int r = 0; r < kMaxOut; ++r) q.tab[c][r] = GfTab{0, 0, 0, 0, 0};
           q.pb[c] = -1;
         }
-        q.npb = p.C;
         q.C = cs;
+        (void)hipGetLastError();
         const int prc = launch_encode_ct<P, VEC>(q, s, typename EncodeShapes<P>::type{});
         if (prc != -1) return prc;
       }
@@ -1698,35 +1722,8 @@ int launch_rows_c(const RowsPlan& p, hipStream_t s) {
       };
       const int rc = ct(p);
       if (rc != -1) return rc;
-      // Pad to the nearest instantiated (NM, NX) with at most kPadRows rows
-      // added in all (a codec without its own ReconstOne shape: 11+4, 13+4,
-      // 9+3, ...): padding GF rows repeat msrc[0] with zero tables, padding
-      // XOR rows repeat xsrc[0] (or msrc[0]) with mask 0.
-      static constexpr int kShapes[][2] = {{12, 4}, {4, 4}, {6, 3}, {8, 2}, {8, 3}, {10, 3},
-                                           {10, 4}, {12, 6}, {14, 4}, {14, 5}, {16, 5},
-                                           {16, 6}, {20, 6}, {20, 7}, {10, 10}};
-      int bm = -1, bx = -1;
-      for (const auto& sh : kShapes) {
-        const int add = (sh[0] - p.NM) + (sh[1] - p.NX);
-        if (sh[0] < p.NM || sh[1] < p.NX || add == 0 || add > kPadRows) continue;
-        if (p.len >= (256u << 10) && sh[0] + sh[1] > 22) continue;
-        if (bm < 0 || add < (bm - p.NM) + (bx - p.NX)) bm = sh[0], bx = sh[1];
-      }
-      if (bm > 0 && p.NM > 0 && !pad_disabled()) {
-        RowsPlan q = p;
-        for (int m = p.NM; m < bm; ++m) {
-          q.msrc[m] = p.msrc[0];
-          for (int r = 0; r < kMaxOut; ++r) q.tab[m][r] = GfTab{0, 0, 0, 0, 0};
-        }
-        for (int x = p.NX; x < bx; ++x) {
-          q.xsrc[x] = p.NX > 0 ? p.xsrc[0] : p.msrc[0];
-          q.xmask[x] = 0;
-        }
-        q.NM = bm;
-        q.NX = bx;
-        const int prc = ct(q);
-        if (prc != -1) return prc;
-      }
+      // (Padding to the nearest (NM, NX) instantiation, as Encode does, lost
+      // 0.5-7% against the runtime kernel: profiles/r03_pad_ab.log.)
     }
   }
   return launch_rows_t<R, kDyn, kDyn, ACC, VEC>(p, s);

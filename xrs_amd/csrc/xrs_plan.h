@@ -52,8 +52,6 @@ struct PairPlan {
   int8_t pb[kMaxSrc];  // piggyback target output of source c's a-half, or -1
   bool encode_xs;      // whole Encode in one launch: source c = data c, and c's
                        // a-half rides on output 1 + c % (P-1) (the XORSet)
-  int npb;             // set by the launcher: sources past npb are padding (zero
-                       // tables, no piggyback); 0 = none
   uint64_t half;       // H = size/2 bytes
   uint64_t n_stripes;
   uint64_t off0, end;  // byte range [off0, end) of each half (set by launch_pair)

@@ -625,7 +625,8 @@ def test_padded_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, p):
         torch.cuda.synchronize()
         xrs_amd.trace_kernels(False)
         names = list(xrs_amd.traced_kernels())
-        if size == 4096:  # compile-time counts (pair_kernel<p, C, ...>) vs runtime (-1)
+        if size == 4096:  # compile-time counts (pair_kernel<p, C, ...>) vs runtime (-1);
+            # padding applies to halves up to 4 KiB only
             assert (f"pair_kernel<{p}, -1," in names[0]) == (mode == "nopad"), names
         ref = host.copy()
         o.encode_batch(ref, size, n)

@@ -36,7 +36,10 @@ def _notes(tmp_path):
     if not os.path.exists(os.path.join(LLVM, "llvm-readelf")):
         pytest.skip("ROCm LLVM tools not available")
     fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB], check=True)
+    # (an output file is named so that objcopy leaves the library untouched:
+    # with none it rewrites its input in place)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB,
+                    str(tmp_path / "discard.so")], check=True)
     subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
                     f"--output={co}", "--unbundle"], check=True)

@@ -1544,7 +1544,7 @@ int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int
 // guard on the piggyback instead raised the 12+4 Encode from 170 to 258
 // VGPRs).
 constexpr int kPadRows = 3;
-constexpr uint64_t kZeroRowBytes = 16u << 20;  // vects up to 16 MiB pad; larger run the runtime kernel
+constexpr uint64_t kZeroRowBytes = 1u << 20;  // >= a whole vect of every padded launch
 
 // Device address of kZeroRowBytes zero bytes on the current device (made
 // once per device, never freed: a launch in flight may read it), or 0.
@@ -1595,8 +1595,11 @@ int launch_pair_c(const PairPlan& p, hipStream_t s) {
       const int rc = launch_encode_ct<P, VEC>(p, s, typename EncodeShapes<P>::type{});
       if (rc != -1) return rc;
       const int cs = pad_count(p.C, typename EncodeShapes<P>::type{});
-      const uint64_t z = (cs > 0 && p.C > 0 && 2 * p.half <= kZeroRowBytes && !pad_disabled())
-                             ? zero_rows() : 0;
+      // Halves up to 4 KiB only: Encode at 4 KiB vects +1..+12% over the
+      // runtime kernel on ten codecs; from 16 KiB vects the runtime kernel is
+      // as fast or faster (-10..+4%, 1 MiB -5..+2%;
+      // profiles/r03_pad_ab2.log, r03_pad_ab3.log).
+      const uint64_t z = (cs > 0 && p.C > 0 && p.half <= 4096 && !pad_disabled()) ? zero_rows() : 0;
       if (z) {
         PairPlan q = p;
         for (int c = p.C; c < cs; ++c) {

@@ -35,16 +35,32 @@ def _notes(tmp_path):
             pytest.skip(f"{tool} not available")
     if not os.path.exists(os.path.join(LLVM, "llvm-readelf")):
         pytest.skip("ROCm LLVM tools not available")
-    fat, co = tmp_path / "fat.bin", tmp_path / "k.co"
+    fat = tmp_path / "fat.bin"
     # (an output file is named so that objcopy leaves the library untouched:
     # with none it rewrites its input in place)
     subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB,
                     str(tmp_path / "discard.so")], check=True)
-    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
-                    f"--output={co}", "--unbundle"], check=True)
-    return subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
-                          capture_output=True, text=True, check=True).stdout
+    # The library links one offload bundle per kernels.hip build part
+    # (XRS_PART): the section holds them back to back, each opening with the
+    # bundle magic.
+    data = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts, i = [], data.find(magic)
+    while i >= 0:
+        starts.append(i)
+        i = data.find(magic, i + 1)
+    assert starts, "no offload bundle in .hip_fatbin"
+    notes = []
+    for n, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
+        part = tmp_path / f"part{n}.bin"
+        part.write_bytes(data[a:b])
+        co = tmp_path / f"k{n}.co"
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}",
+                        f"--output={co}", "--unbundle"], check=True)
+        notes.append(subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
+                                    capture_output=True, text=True, check=True).stdout)
+    return "\n".join(notes)
 
 
 def _kernels(txt):

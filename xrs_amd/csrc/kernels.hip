@@ -35,6 +35,15 @@
 #include "gf256.h"
 #include "xrs_plan.h"
 
+// Build parts: the Makefile compiles this file once per XRS_PART (1: launch
+// trace + pair kernels, 2: staged, 3: update_rows, 4: rows), so the gfx950
+// code generation of the four kernel families runs in parallel.  Without
+// XRS_PART (tools/, the host-sanitizer test build) one unit holds everything.
+#ifndef XRS_PART
+#define XRS_PART 0
+#endif
+#define XRS_HAS_PART(n) (XRS_PART == 0 || XRS_PART == (n))
+
 namespace xrs {
 namespace {
 
@@ -1003,13 +1012,18 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P
   }
 }
 
+}  // namespace
+
 // ============================================================ launch trace
 // Diagnostic record of which kernel instantiations this process launched
 // (xrs_trace_kernels / xrs_traced_kernels): smoke() and the dispatch tests
 // name the kernels they exercised.  Off: one relaxed atomic load per launch.
-std::atomic<bool> g_trace{false};
-std::mutex g_trace_mu;
-std::vector<std::pair<std::string, uint64_t>> g_trace_log;  // (kernel, launches)
+// Shared by every build part (defined in part 1, see the end of the file).
+extern std::atomic<bool> g_trace;
+extern std::mutex g_trace_mu;
+extern std::vector<std::pair<std::string, uint64_t>> g_trace_log;  // (kernel, launches)
+
+namespace {
 
 // Device symbol name -> "pair_kernel<4, 12, false, true, 128, true>" (the
 // name rocprofv3 prints, without namespaces, return type and parameters).
@@ -1812,6 +1826,11 @@ bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len, uint64_t n_str
 
 }  // namespace
 
+#if XRS_HAS_PART(1)
+std::atomic<bool> g_trace{false};
+std::mutex g_trace_mu;
+std::vector<std::pair<std::string, uint64_t>> g_trace_log;
+
 void trace_kernels(bool on) {
   std::lock_guard<std::mutex> g(g_trace_mu);
   if (on) g_trace_log.clear();
@@ -1848,7 +1867,9 @@ int launch_pair(const PairPlan& p0, void* stream) {
     return vec ? launch_pair_p<false, true>(p, s) : launch_pair_p<false, false>(p, s);
   }, pure);
 }
+#endif  // XRS_HAS_PART(1)
 
+#if XRS_HAS_PART(2)
 int launch_staged(const StagedPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStB || p0.nl < 0 ||
@@ -1874,7 +1895,9 @@ int launch_staged(const StagedPlan& p0, void* stream) {
     return vec ? launch_staged_r<true>(p, s) : launch_staged_r<false>(p, s);
   });
 }
+#endif  // XRS_HAS_PART(2)
 
+#if XRS_HAS_PART(3)
 int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.P < 1 || p0.P > kMaxOut || p0.nrows < 1 || p0.nrows > kMaxSrc || (!p0.rows && p0.nrows != 1))
@@ -1885,7 +1908,9 @@ int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
     return vec ? launch_update_rows_p<true>(p, s) : launch_update_rows_p<false>(p, s);
   });
 }
+#endif  // XRS_HAS_PART(3)
 
+#if XRS_HAS_PART(4)
 int launch_rows(const RowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.R < 1 || p0.R > kMaxOut || p0.NM < 0 || p0.NM > kMaxSrc || p0.NX < 0 || p0.NX > kMaxXor)
@@ -1906,5 +1931,7 @@ int launch_rows(const RowsPlan& p0, void* stream) {
     return vec ? launch_rows_r<false, true>(p, s) : launch_rows_r<false, false>(p, s);
   }, pure);
 }
+
+#endif  // XRS_HAS_PART(4)
 
 }  // namespace xrs

@@ -134,7 +134,11 @@ int main(int argc, char** argv) {
   for (int upd = 0; upd < (qonly ? 1 : 2); ++upd)
   for (int threads : tlist) {
     xrs_queue* q = nullptr;
-    if (xrs_queue_new(c, size, 1024, wait_us, &q)) return 4;
+    if (int e = xrs_queue_new(c, size, 1024, wait_us, &q)) {
+      std::printf("xrs_queue_new failed: %d\n", e);
+      std::fflush(stdout);
+      return 4;
+    }
     std::atomic<long> total{0};
     std::atomic<bool> stop{false};
     std::vector<std::thread> th;
@@ -147,7 +151,11 @@ int main(int argc, char** argv) {
         while (!stop.load(std::memory_order_relaxed)) {
           const int rc = upd ? xrs_queue_update(q, p[t % 12], p[(t + 1) % 12], t % 12, p.data() + 12, 4)
                              : xrs_queue_encode(q, p.data(), 16);
-          if (rc) std::abort();
+          if (rc) {
+            std::printf("queue call failed: %d\n", rc);
+            std::fflush(stdout);
+            std::_Exit(5);
+          }
           ++n;
         }
         total += n;
@@ -155,6 +163,19 @@ int main(int argc, char** argv) {
     const double t0 = now();
     std::this_thread::sleep_for(std::chrono::seconds(seconds));
     stop = true;
+    // watchdog: callers that do not all return within 10 s are stuck
+    std::atomic<bool> joined{false};
+    std::thread wd([&] {
+      for (int i = 0; i < 1000 && !joined.load(); ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      if (joined.load()) return;
+      uint64_t st[4] = {0, 0, 0, 0};
+      xrs_queue_stats(q, st);
+      std::printf("HANG: callers or xrs_queue_free stuck 10 s after stop (batches %llu, stripes %llu)\n",
+                  (unsigned long long)st[0], (unsigned long long)st[1]);
+      std::fflush(stdout);
+      std::_Exit(6);
+    });
     for (auto& x : th) x.join();
     const double dt = now() - t0;
     uint64_t st[4] = {0, 0, 0, 0};
@@ -168,6 +189,8 @@ int main(int argc, char** argv) {
                 st[2] / nb / 1e3, st[3] / nb / 1e3);
     std::fflush(stdout);
     xrs_queue_free(q);
+    joined = true;
+    wd.join();
   }
   xrs_free(c);
   std::fflush(stdout);

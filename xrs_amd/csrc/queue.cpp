@@ -5,23 +5,42 @@
 // stripe is latency bound, so the queue coalesces concurrent per-stripe calls
 // into device batches:
 //
-//   caller thread: reserve a slot in the open batch -> copy its vects into the
-//     batch's pinned staging (callers copy in parallel) -> wait -> copy its
-//     outputs back -> release the slot.
-//   worker threads (XRS_QUEUE_WORKERS, default 2): run a batch when it is
-//     full, or when it has waited max_wait_us with every reserved slot
-//     filled: one H2D of the whole batch, one kernel over all its stripes,
-//     one D2H, on the batch's own stream.
+//   caller thread: reserve a slot in the open batch (under the queue mutex,
+//     a few hundred ns) -> copy its vects into the batch's pinned staging
+//     (callers copy in parallel) -> sleep on the batch's completion word (a
+//     futex) -> copy its outputs back -> release the slot.
+//   worker threads (XRS_QUEUE_WORKERS, default 2): take a batch, wait for its
+//     slots to be staged, run it, and spin on the stream until it is done;
+//     then one futex wake releases every caller of the batch at once.
 //     Batches of up to XRS_QUEUE_ZC_MAX bytes (default 4 MiB) skip both
 //     copies: the kernel reads and writes the pinned, device-mapped staging
-//     over PCIe (measured faster than DMA at these sizes).
+//     over PCIe (measured faster than DMA at these sizes);
+//     larger ones get one H2D of the whole batch, one kernel and one D2H on
+//     the batch's own stream.
+//
+// When a worker closes the open batch (XRS_QUEUE_POLICY):
+//   "free" (default): as soon as a worker is free, so each batch holds the
+//     calls that arrived while the previous ones ran (sizes follow the load);
+//   "timer": when it is full, when nothing is in flight (a lone caller does
+//     not wait for company), or after max_wait_us.
+// Completion latency, not bandwidth, bounds per-stripe calls at 4 KiB
+// (a 28-stripe batch is 1.8 MB of PCIe traffic, ~35 us at 55 GB/s): the
+// round-2 queue woke a batch's callers through one condition variable and
+// mutex (a chain of hand-offs, one context switch per caller) and waited on
+// the stream with a blocking sync; both are gone.
 //
 // Every stripe's arithmetic is the batched device path (encode_dev /
 // reconst_one_dev); results are bit-identical to the per-stripe calls.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -50,6 +69,31 @@ constexpr int kMaxWorkers = 8;  // batches in flight at once: XRS_QUEUE_WORKERS,
 constexpr int kBatches = kMaxWorkers + 2;  // staging buffers: one per worker + two filling
 constexpr size_t kMaxBatchBytes = 64u << 20;
 
+// A 32-bit futex word: waiters sleep in the kernel until it changes, and one
+// wake releases all of them together.
+static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
+void futex_wait(std::atomic<uint32_t>* w, uint32_t v) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+void futex_wake_all(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr,
+          0);
+}
+
+// Spin (pause) for about `spin_ns`, then yield, until pred() holds.
+template <class F>
+void spin_until(F pred, uint64_t spin_ns) {
+  const auto t0 = Clock::now();
+  for (int i = 0; !pred(); ++i) {
+    if ((i & 63) == 63 &&
+        static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0)
+                                  .count()) > spin_ns)
+      std::this_thread::yield();
+    else
+      _mm_pause();
+  }
+}
+
 enum State { FREE, OPEN, CLOSED, RUNNING, DONE };
 
 struct Batch {
@@ -59,15 +103,18 @@ struct Batch {
   int32_t* rows = nullptr;      // pinned, mapped: Update's data row per slot
   int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
   hipStream_t stream = nullptr;
+  // guarded by the queue mutex
   State state = FREE;
   int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows),
                  // 2 + d: reconst(pat_has, pat_need), 3 + d: replace(pat_has = rows)
   std::vector<int> pat_has, pat_need;  // Reconst pattern of the batch
-  size_t reserved = 0, filled = 0, released = 0;
-  uint64_t gen = 0;
-  int err = 0;
+  size_t reserved = 0;
   Clock::time_point opened;
-  std::condition_variable done;  // this batch's waiters only (no thundering herd)
+  // lock-free: slots staged / slots released, and the completion word (+1
+  // when the batch's results are in staging; err and n are written first)
+  std::atomic<uint32_t> filled{0}, released{0}, done{0};
+  size_t n = 0;  // slots of the closed batch
+  int err = 0;
 };
 
 }  // namespace
@@ -79,18 +126,20 @@ struct xrs_queue {
   std::chrono::microseconds max_wait{50};
   Batch b[kBatches];
   int open = -1;
-  int running = 0;  // batches being run by workers
-  int active = 0;   // callers inside submit() (xrs_queue_free waits for 0)
+  int running = 0;  // batches taken by workers (guarded by mu)
+  std::atomic<int> active{0};  // callers inside submit() (xrs_queue_free waits for 0)
   bool stop = false;
   // statistics (guarded by mu): batches run, stripes run, device time
-  // (launch to stream sync) and queueing time (open to launch) summed over
-  // batches, in ns
+  // (launch to completion seen) and queueing time (open to launch) summed
+  // over batches, in ns
   uint64_t st_batches = 0, st_stripes = 0, st_run_ns = 0, st_wait_ns = 0;
   std::mutex mu;
   std::condition_variable cv_work, cv_free;
   std::thread worker[kMaxWorkers];
   int n_workers = 2, n_batches = 4;
-  bool eager = false;  // XRS_QUEUE_POLICY=free: a free worker runs the open batch at once
+  bool timer = false;       // XRS_QUEUE_POLICY=timer
+  bool block_sync = false;  // XRS_QUEUE_SYNC=block: hipStreamSynchronize (A/B)
+  uint64_t spin_ns = 20000;  // worker spin before yielding
 
   // One copy between a caller's buffer and its staged stripe: `len` bytes at
   // staging row `row` (row * size + off) <-> host + off.
@@ -100,15 +149,26 @@ struct xrs_queue {
     size_t off, len;
   };
 
-  void run(int i);
+  int run(Batch& bt);
   void work();
+  void close_open() {  // (mu held)
+    b[open].state = CLOSED;
+    b[open].n = b[open].reserved;
+    open = -1;
+    cv_work.notify_one();
+  }
+  void leave() {
+    if (active.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (stop) cv_free.notify_all();
+    }
+  }
   int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1,
              const std::vector<int>* has = nullptr, const std::vector<int>* need = nullptr);
 };
 
-void xrs_queue::run(int i) {
-  Batch& bt = b[i];
-  const size_t n = bt.reserved;
+int xrs_queue::run(Batch& bt) {
+  const size_t n = bt.n;
   // Encode: only the data rows go up and only the parity rows come back (one
   // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back;
   // Update(row): parity rows, old and new up (rows [0, p+2)), parity back.
@@ -153,11 +213,15 @@ void xrs_queue::run(int i) {
       hipMemcpy2DAsync(bt.host + dn_off, stripe_bytes, bt.dev + dn_off, stripe_bytes, dn_len, n,
                        hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
-  if (hipStreamSynchronize(bt.stream) != hipSuccess && !e) e = XRS_ERR_HIP;
-  std::lock_guard<std::mutex> lk(mu);
-  bt.err = e;
-  bt.state = DONE;
-  bt.done.notify_all();
+  // Completion: spin on the stream (a blocking sync sleeps on an interrupt).
+  hipError_t q;
+  if (block_sync) {
+    q = hipStreamSynchronize(bt.stream);
+  } else {
+    spin_until([&] { return (q = hipStreamQuery(bt.stream)) != hipErrorNotReady; }, spin_ns);
+  }
+  if (q != hipSuccess && !e) e = XRS_ERR_HIP;
+  return e;
 }
 
 void xrs_queue::work() {
@@ -170,21 +234,20 @@ void xrs_queue::work() {
     for (int i = 0; i < n_batches && pick < 0; ++i) {
       Batch& bt = b[i];
       if (bt.state == OPEN || bt.state == CLOSED) pending = true;
-      if (bt.state == CLOSED && bt.filled == bt.reserved) pick = i;
-      if (bt.state == OPEN && bt.filled == bt.reserved && bt.reserved > 0) {
-        // A small batch runs at once when no batch is in flight (a lone
-        // caller does not wait for company); otherwise, and for large
-        // stripes (PCIe-bound, where bigger batches measured faster), it
-        // grows until max_wait has passed.
-        const auto due = bt.opened + max_wait;
-        const bool small = bt.reserved * stripe_bytes <= zc_max;
-        // (stopping: drain, every caller already in gets its result)
-        if ((running == 0 && small) || eager || stop || Clock::now() >= due) {
-          bt.state = CLOSED;
-          if (open == i) open = -1;
+      if (bt.state == CLOSED) pick = i;
+      if (bt.state == OPEN && bt.reserved > 0) {
+        bool go = !timer || stop;  // (stopping: drain, every caller already in gets its result)
+        if (!go) {
+          // timer: a small batch runs at once when nothing is in flight;
+          // otherwise, and for large stripes (PCIe-bound, where bigger
+          // batches measured faster), it grows until max_wait has passed.
+          const auto due = bt.opened + max_wait;
+          go = (running == 0 && bt.reserved * stripe_bytes <= zc_max) || Clock::now() >= due;
+          if (!go) next = std::min(next, due);
+        }
+        if (go) {
+          close_open();
           pick = i;
-        } else {
-          next = std::min(next, due);
         }
       }
     }
@@ -193,22 +256,31 @@ void xrs_queue::work() {
       cv_work.wait_until(lk, next);
       continue;
     }
-    b[pick].state = RUNNING;
+    Batch& bt = b[pick];
+    bt.state = RUNNING;
     ++running;
-    const size_t n = b[pick].reserved;
+    const size_t n = bt.n;
+    lk.unlock();
+    // the batch's callers are still copying in (a few us at 4 KiB)
+    spin_until([&] { return bt.filled.load(std::memory_order_acquire) == n; }, spin_ns);
     const auto t0 = Clock::now();
     const uint64_t waited =
-        std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - b[pick].opened).count();
-    lk.unlock();
-    run(pick);
+        std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - bt.opened).count();
+    const int e = run(bt);
     const uint64_t ran =
         std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
     lk.lock();
+    bt.err = e;
+    bt.state = DONE;
     --running;
     ++st_batches;
     st_stripes += n;
     st_run_ns += ran;
     st_wait_ns += waited;
+    lk.unlock();
+    bt.done.fetch_add(1, std::memory_order_release);
+    futex_wake_all(&bt.done);
+    lk.lock();
   }
 }
 
@@ -217,25 +289,22 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   auto same_pattern = [&](const Batch& bt) {
     return !has || (bt.pat_has == *has && bt.pat_need == *need);
   };
-  int bi;
+  Batch* bp;
   size_t slot;
-  uint64_t gen;
+  uint32_t seq;
   {
     std::unique_lock<std::mutex> lk(mu);
-    ++active;
+    if (stop) return XRS_ERR_INVALID_ARG;
+    active.fetch_add(1, std::memory_order_relaxed);
     for (;;) {
       if (stop) {
-        --active;
-        cv_free.notify_all();
+        lk.unlock();
+        leave();
         return XRS_ERR_INVALID_ARG;
       }
       if (open >= 0 && b[open].key == key && b[open].reserved < max_batch && same_pattern(b[open]))
         break;
-      if (open >= 0) {  // different op or full: close it, the worker runs it
-        b[open].state = CLOSED;
-        open = -1;
-        cv_work.notify_all();
-      }
+      if (open >= 0) close_open();  // different op or full: the worker runs it
       int f = -1;
       for (int i = 0; i < n_batches && f < 0; ++i)
         if (b[i].state == FREE) f = i;
@@ -246,7 +315,9 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       Batch& nb = b[f];
       nb.state = OPEN;
       nb.key = key;
-      nb.reserved = nb.filled = nb.released = 0;
+      nb.reserved = nb.n = 0;
+      nb.filled.store(0, std::memory_order_relaxed);
+      nb.released.store(0, std::memory_order_relaxed);
       nb.err = 0;
       nb.opened = Clock::now();
       if (has) {
@@ -254,41 +325,35 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
         nb.pat_need = *need;
       }
       open = f;
+      if (!timer) cv_work.notify_one();  // a free worker takes it at once
     }
-    bi = open;
-    slot = b[bi].reserved++;
-    gen = b[bi].gen;
-    if (b[bi].reserved == max_batch) {
-      b[bi].state = CLOSED;
-      open = -1;
-    }
+    bp = &b[open];
+    slot = bp->reserved++;
+    seq = bp->done.load(std::memory_order_relaxed);
+    if (bp->reserved == max_batch) close_open();
   }
-  Batch& bt = b[bi];
+  Batch& bt = *bp;
   uint8_t* st = bt.host + slot * stripe_bytes;
   if (row >= 0) bt.rows[slot] = row;
   for (const Piece& pc : in)
     std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
-  int err;
-  {
-    std::unique_lock<std::mutex> lk(mu);
-    // Wake a worker only when this fill makes the batch runnable (closed, or
-    // open with every reservation staged: the worker's timer then applies).
-    if (++bt.filled == bt.reserved) cv_work.notify_one();
-    bt.done.wait(lk, [&] { return bt.gen == gen && bt.state == DONE; });
-    err = bt.err;
+  bt.filled.fetch_add(1, std::memory_order_release);
+  if (timer) {
+    // the timer policy's worker may be asleep on a batch that is now staged
+    std::lock_guard<std::mutex> lk(mu);
+    cv_work.notify_one();
   }
+  while (bt.done.load(std::memory_order_acquire) == seq) futex_wait(&bt.done, seq);
+  const int err = bt.err;
   if (!err)
     for (const Piece& pc : out)
       std::memcpy(pc.host + pc.off, st + static_cast<size_t>(pc.row) * size + pc.off, pc.len);
-  {
+  if (bt.released.fetch_add(1, std::memory_order_acq_rel) + 1 == bt.n) {
     std::lock_guard<std::mutex> lk(mu);
-    if (++bt.released == bt.reserved) {
-      bt.state = FREE;
-      bt.gen++;
-    }
-    --active;
+    bt.state = FREE;
     cv_free.notify_all();
   }
+  leave();
   return err;
 }
 
@@ -318,7 +383,11 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   if (wv && *wv) q->n_workers = std::max(1, std::min(kMaxWorkers, std::atoi(wv)));
   q->n_batches = q->n_workers + 2;
   const char* pv = std::getenv("XRS_QUEUE_POLICY");
-  q->eager = pv && std::strcmp(pv, "free") == 0;
+  q->timer = pv && std::strcmp(pv, "timer") == 0;
+  const char* sv = std::getenv("XRS_QUEUE_SYNC");
+  q->block_sync = sv && std::strcmp(sv, "block") == 0;
+  const char* nv = std::getenv("XRS_QUEUE_SPIN_NS");
+  if (nv && *nv) q->spin_ns = std::strtoull(nv, nullptr, 0);
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
@@ -360,7 +429,7 @@ void xrs_queue_free(xrs_queue* q) {
     q->stop = true;
     q->cv_work.notify_all();
     q->cv_free.notify_all();
-    q->cv_free.wait(lk, [q] { return q->active == 0; });
+    q->cv_free.wait(lk, [q] { return q->active.load() == 0; });
   }
   for (auto& w : q->worker)
     if (w.joinable()) w.join();

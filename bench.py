@@ -32,6 +32,9 @@ After the headline timed region, the same line carries:
     per-rank times;
   * "host_e2e": the host-resident path (shards start and end in pinned host
     memory, xrs_*_host, PCIe-inclusive) on every rank at once;
+  * "per_stripe_queue" (N = 1): the reference's per-stripe Encode call from
+    32 caller threads through the batching queue (tools/sync_bench child,
+    host-resident 4 KiB stripes, PCIe-inclusive);
   * "xgmi_repair" (two or more visible GPUs): rank 0 (in a child process)
     rebuilds a data shard with half of its need set on the peer GPU (xGMI
     reads), checked bit for bit against the rebuild from local shards.
@@ -271,6 +274,8 @@ def parse_args(argv=None):
     ap.add_argument("--config5-steps", type=int, default=20)  # ~3.5 s of GPU work
     ap.add_argument("--host-mib", type=int, default=1024,
                     help="MiB per host-resident batch for the host_e2e key (0: skip)")
+    ap.add_argument("--queue-callers", type=int, nargs="*", default=[32],
+                    help="caller threads for the per_stripe_queue key (N = 1 only; none: skip)")
     ap.add_argument("--xgmi-stripes", type=int, default=64,
                     help="1 MiB stripes for the xgmi_repair key (0: skip)")
     ap.add_argument("--xgmi-child", type=int, default=None, help=argparse.SUPPRESS)
@@ -629,6 +634,32 @@ def run_xgmi_child(args, device: int, ndev: int):
     return json.loads(lines[-1])
 
 
+def per_stripe_queue(args):
+    """The reference's call pattern (one Encode per stripe, xrs_test.go:498-521)
+    from T concurrent caller threads through the batching queue
+    (xrs_queue_encode, xrs_amd/csrc/queue.cpp): tools/sync_bench, a C++ child
+    process, 2 s per caller count, host-resident 12+4 stripes of 4 KiB.  Rate
+    in the reference's bytes (16 * S per stripe), PCIe-inclusive; not part of
+    `value`."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "sync_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/sync_bench not built (build() makes it)"}
+    cmd = [exe, "4096", "queue", "50"] + [str(t) for t in args.queue_callers]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 120 s"}
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}", "stdout_tail": r.stdout[-400:]}
+    return {"api": "xrs_queue_encode", "vect_bytes": 4096, "codec": "12+4",
+            "by_callers": {str(x["threads"]): {k: x[k] for k in (
+                "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch",
+                "wait_us_per_batch")} for x in lines}}
+
+
 def xgmi_child(args) -> int:
     R = Rank(xdist.World(0, 1, args.xgmi_child, False), "none")
     print(json.dumps(xgmi_repair(R, args)), flush=True)
@@ -666,6 +697,10 @@ def run_rank(args, w):
     if args.config5_stripes > 0:
         c5 = config5(R, args)
     he = host_e2e(R, args) if args.host_mib > 0 else None
+    pq = None
+    if w.rank == 0 and w.world == 1 and args.queue_callers:
+        log("per-stripe calls through the batching queue ...")
+        pq = per_stripe_queue(args)
     xg = None
     if args.xgmi_stripes > 0:
         xdist.barrier()
@@ -722,6 +757,7 @@ def run_rank(args, w):
             "cpu_baseline": cpu,
             "config5": c5,
             "host_e2e": he,
+            "per_stripe_queue": pq,
             "xgmi_repair": xg,
         }
         print(json.dumps(out), flush=True)

@@ -271,6 +271,11 @@ size_t xrs_queue_batch_stripes(const xrs_queue *q);
  * out[2] ns from each batch's launch to its completion, out[3] ns each batch
  * waited between opening and launch (summed over batches). */
 int xrs_queue_stats(xrs_queue *q, uint64_t out[4]);
+/* Diagnostics: the queue's state (per staging batch: state, slots reserved /
+ * staged / released, launches and the completion word) as text into buf
+ * (NUL-terminated, truncated to cap); returns the full length.  Takes the
+ * queue lock only if it is free within 10 ms. */
+size_t xrs_queue_dump(xrs_queue *q, char *buf, size_t cap);
 
 #ifdef __cplusplus
 }

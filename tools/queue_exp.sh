@@ -1,19 +1,27 @@
 #!/bin/bash
-# Batching-queue experiments (tools/sync_bench): CONFIGS of
-# policy:workers:sync:spin_ns, THREADS callers, 4 KiB vects.
+# Batching-queue experiments (tools/sync_bench): the queue's GPU tests, then
+# CONFIGS of policy:launchers:inflight[:engine], THREADS callers, SIZES vects
+# (engine 0: XRS_QUEUE_ENGINE=0, every batch launched).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-CONFIGS=${CONFIGS:-"free:6:block:0 free:6:spin:2000"}
-THREADS=${THREADS:-"16 32 48"}
-SIZE=${SIZE:-4096}
+if [ "${QTEST:-1}" = 1 ]; then
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_queue.py -x -q -p no:cacheprovider \
+    --timeout 120 --timeout-method thread > gpurun_out/q_pytest.log 2>&1
+  rc=$?; tail -3 gpurun_out/q_pytest.log; [ $rc -eq 0 ] || exit $rc
+fi
+CONFIGS=${CONFIGS:-"free:1:2 free:1:3 free:1:4 free:2:3 free:2:6"}
+THREADS=${THREADS:-"1 8 16 32 48"}
+SIZES=${SIZES:-4096}
+for size in $SIZES; do
 for cfg in $CONFIGS; do
-  IFS=: read -r pol w sync spin <<< "$cfg"
-  echo "policy=$pol workers=$w sync=$sync spin_ns=$spin"
-  XRS_QUEUE_POLICY=$pol XRS_QUEUE_WORKERS=$w XRS_QUEUE_SYNC=$sync XRS_QUEUE_SPIN_NS=$spin \
-    timeout -k 10 60 tools/sync_bench $SIZE queue 50 $THREADS
+  IFS=: read -r pol w inf eng <<< "$cfg"
+  echo "size=$size policy=$pol launchers=$w inflight=$inf engine=${eng:-1}"
+  XRS_QUEUE_POLICY=$pol XRS_QUEUE_WORKERS=$w XRS_QUEUE_INFLIGHT=$inf XRS_QUEUE_ENGINE=${eng:-1} \
+    timeout -k 10 90 tools/sync_bench $size queue 50 $THREADS
   rc=$?
   echo "rc=$rc"
-  [ $rc -eq 0 ] || break
+  [ $rc -eq 0 ] || break 2
+done
 done > gpurun_out/qexp_ab.log 2>&1
 cat gpurun_out/qexp_ab.log

@@ -173,6 +173,9 @@ int main(int argc, char** argv) {
       xrs_queue_stats(q, st);
       std::printf("HANG: callers or xrs_queue_free stuck 10 s after stop (batches %llu, stripes %llu)\n",
                   (unsigned long long)st[0], (unsigned long long)st[1]);
+      static char dump[8192];
+      xrs_queue_dump(q, dump, sizeof dump);
+      std::printf("%s", dump);
       std::fflush(stdout);
       std::_Exit(6);
     });
@@ -188,6 +191,12 @@ int main(int argc, char** argv) {
                 size, threads, total / dt, total * (upd ? 10.0 : 16.0) * size / dt / (1 << 30), (unsigned long long)st[0], st[1] / nb,
                 st[2] / nb / 1e3, st[3] / nb / 1e3);
     std::fflush(stdout);
+    if (std::getenv("XRS_QUEUE_DUMP")) {
+      static char dump[8192];
+      xrs_queue_dump(q, dump, sizeof dump);
+      std::printf("%s", dump);
+      std::fflush(stdout);
+    }
     xrs_queue_free(q);
     joined = true;
     wd.join();

@@ -118,6 +118,7 @@ def _load():
         "xrs_queue_replace": ([P, PP, IP, I, PP, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
+        "xrs_queue_dump": ([P, ctypes.c_char_p, Z], Z),
         "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
         "xrs_group_free": ([P], None),
         "xrs_group_size": ([P], I),

@@ -9,25 +9,32 @@
 //     a few hundred ns) -> copy its vects into the batch's pinned staging
 //     (callers copy in parallel) -> sleep on the batch's completion word (a
 //     futex) -> copy its outputs back -> release the slot.
-//   worker threads (XRS_QUEUE_WORKERS, default 2): take a batch, wait for its
-//     slots to be staged, run it, and spin on the stream until it is done;
-//     then one futex wake releases every caller of the batch at once.
+//   launcher threads (XRS_QUEUE_WORKERS, default 1): take a batch, wait for
+//     its slots to be staged, enqueue it on the batch's own stream followed by
+//     a write of the batch's sequence number to a pinned host word, and move
+//     on: a launcher never waits for the GPU.
 //     Batches of up to XRS_QUEUE_ZC_MAX bytes (default 4 MiB) skip both
 //     copies: the kernel reads and writes the pinned, device-mapped staging
 //     over PCIe (measured faster than DMA at these sizes);
-//     larger ones get one H2D of the whole batch, one kernel and one D2H on
-//     the batch's own stream.
+//     larger ones get one H2D of the whole batch, one kernel and one D2H.
+//   completion thread: spins on the in-flight batches' host words (no HIP
+//     call on the fast path; hipStreamQuery now and then catches a failed
+//     stream), and for each finished batch bumps its futex word: one wake
+//     releases every caller of the batch at once.
 //
-// When a worker closes the open batch (XRS_QUEUE_POLICY):
-//   "free" (default): as soon as a worker is free, so each batch holds the
-//     calls that arrived while the previous ones ran (sizes follow the load);
+// When a launcher closes the open batch (XRS_QUEUE_POLICY):
+//   "free" (default): as soon as fewer than XRS_QUEUE_INFLIGHT (default 4)
+//     batches are in flight, so each batch holds the calls that arrived
+//     while the previous ones ran (sizes follow the load);
 //   "timer": when it is full, when nothing is in flight (a lone caller does
 //     not wait for company), or after max_wait_us.
-// Completion latency, not bandwidth, bounds per-stripe calls at 4 KiB
-// (a 28-stripe batch is 1.8 MB of PCIe traffic, ~35 us at 55 GB/s): the
-// round-2 queue woke a batch's callers through one condition variable and
-// mutex (a chain of hand-offs, one context switch per caller) and waited on
-// the stream with a blocking sync; both are gone.
+// Completion latency, not bandwidth, bounds per-stripe calls at 4 KiB (a
+// 28-stripe batch is 1.8 MB of PCIe traffic, ~35 us at 55 GB/s).  Measured on
+// MI355X (tools/qlat_probe.hip, profiles/r03_queue_latency_probe.log): a
+// spinning hipStreamQuery sees an empty kernel done 12-16 us after the launch
+// call, a host word written by the stream 7.4 us after; the round-2 queue also
+// woke a batch's callers through one condition variable and mutex (a chain of
+// hand-offs, one context switch per caller).
 //
 // Every stripe's arithmetic is the batched device path (encode_dev /
 // reconst_one_dev); results are bit-identical to the per-stripe calls.
@@ -45,10 +52,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "xrs_hip.h"
+#include "xrs_plan.h"
 
 namespace xrs_detail {
 int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
@@ -59,15 +68,21 @@ int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi);
 int codec_device(const xrs_codec* x);
 int codec_d(const xrs_codec* x);
 int codec_p(const xrs_codec* x);
+int capture_plans(const xrs_codec* x, uint8_t* base, size_t size, size_t stripe_stride,
+                  std::vector<xrs::PairPlan>* enc, std::vector<xrs::RowsPlan>* rec,
+                  std::vector<int>* rec_count);
 }  // namespace xrs_detail
 
 using Clock = std::chrono::steady_clock;
 
 namespace {
 
-constexpr int kMaxWorkers = 8;  // batches in flight at once: XRS_QUEUE_WORKERS, default 2
-constexpr int kBatches = kMaxWorkers + 2;  // staging buffers: one per worker + two filling
+constexpr int kMaxWorkers = 8;   // launcher threads: XRS_QUEUE_WORKERS, default 1
+constexpr int kBatches = 16;     // staging buffers: XRS_QUEUE_BATCHES, default in-flight + 2
+constexpr int kFlagStride = 16;  // uint32 words between batches' host words (64 B)
 constexpr size_t kMaxBatchBytes = 64u << 20;
+constexpr uint64_t kStuckNs = 20000000;  // in flight this long: ask the stream for errors
+constexpr int64_t kEngineIdleNs = 2000000;  // no post for 2 ms: the resident engine stops
 
 // A 32-bit futex word: waiters sleep in the kernel until it changes, and one
 // wake releases all of them together.
@@ -80,21 +95,24 @@ void futex_wake_all(std::atomic<uint32_t>* w) {
           0);
 }
 
+uint64_t ns_since(Clock::time_point t0) {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+}
+
 // Spin (pause) for about `spin_ns`, then yield, until pred() holds.
 template <class F>
 void spin_until(F pred, uint64_t spin_ns) {
   const auto t0 = Clock::now();
   for (int i = 0; !pred(); ++i) {
-    if ((i & 63) == 63 &&
-        static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0)
-                                  .count()) > spin_ns)
+    if ((i & 63) == 63 && ns_since(t0) > spin_ns)
       std::this_thread::yield();
     else
       _mm_pause();
   }
 }
 
-enum State { FREE, OPEN, CLOSED, RUNNING, DONE };
+enum State { FREE, OPEN, CLOSED, LAUNCHING, INFLIGHT, DONE };
 
 struct Batch {
   uint8_t* host = nullptr;      // pinned staging, compact [stripe][shard][size]
@@ -103,13 +121,17 @@ struct Batch {
   int32_t* rows = nullptr;      // pinned, mapped: Update's data row per slot
   int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
   hipStream_t stream = nullptr;
+  volatile uint32_t* flag = nullptr;  // pinned host word the stream writes `launches` to
+  uint32_t* flag_dev = nullptr;
+  uint32_t launches = 0;
+  bool engine = false;  // the last launch went to the resident engine
   // guarded by the queue mutex
   State state = FREE;
   int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows),
                  // 2 + d: reconst(pat_has, pat_need), 3 + d: replace(pat_has = rows)
   std::vector<int> pat_has, pat_need;  // Reconst pattern of the batch
   size_t reserved = 0;
-  Clock::time_point opened;
+  Clock::time_point opened, launched;
   // lock-free: slots staged / slots released, and the completion word (+1
   // when the batch's results are in staging; err and n are written first)
   std::atomic<uint32_t> filled{0}, released{0}, done{0};
@@ -125,21 +147,42 @@ struct xrs_queue {
   size_t size = 0, stripe_bytes = 0, max_batch = 1, zc_max = 0;
   std::chrono::microseconds max_wait{50};
   Batch b[kBatches];
+  uint32_t* flags = nullptr;  // pinned, mapped: kFlagStride words per batch
   int open = -1;
-  int running = 0;  // batches taken by workers (guarded by mu)
+  int in_flight = 0;  // batches launching or in flight (guarded by mu)
+  std::atomic<uint32_t> inflight_bits{0};  // bit i: batch i waits for its host word
   std::atomic<int> active{0};  // callers inside submit() (xrs_queue_free waits for 0)
-  bool stop = false;
+  bool stop = false, comp_stop = false;
   // statistics (guarded by mu): batches run, stripes run, device time
   // (launch to completion seen) and queueing time (open to launch) summed
   // over batches, in ns
   uint64_t st_batches = 0, st_stripes = 0, st_run_ns = 0, st_wait_ns = 0;
   std::mutex mu;
-  std::condition_variable cv_work, cv_free;
-  std::thread worker[kMaxWorkers];
-  int n_workers = 2, n_batches = 4;
-  bool timer = false;       // XRS_QUEUE_POLICY=timer
-  bool block_sync = false;  // XRS_QUEUE_SYNC=block: hipStreamSynchronize (A/B)
-  uint64_t spin_ns = 20000;  // worker spin before yielding
+  std::condition_variable cv_work, cv_free, cv_comp;
+  std::thread worker[kMaxWorkers], completer;
+  int n_workers = 1, n_batches = 6, max_inflight = 4;
+  bool timer = false;        // XRS_QUEUE_POLICY=timer
+  uint64_t spin_ns = 20000;  // launcher spin (staging fills) before yielding
+  uint64_t comp_spin_ns = 200000;  // completion thread spin before yielding
+  // Resident engine (kernels.hip part 5): 12+4 codecs, vect sizes that are
+  // multiples of 32, zero-copy Encode / ReconstOne batches.  Started by the
+  // first such batch, stopped after kEngineIdleNs without one (and at
+  // teardown).  Off unless XRS_QUEUE_ENGINE=1: measured slower than launching
+  // (profiles/r03_queue_engine_ab.log).
+  bool eng_ok = false;
+  std::atomic<bool> eng_running{false};
+  void* eng_args = nullptr;
+  xrs::EngineCtl* eng_ctl = nullptr;
+  xrs::EngineCtl* eng_ctl_dev = nullptr;
+  xrs::EngineDesc* eng_ring = nullptr;
+  xrs::EngineDesc* eng_ring_dev = nullptr;
+  uint32_t* eng_count = nullptr;
+  hipStream_t eng_stream = nullptr;
+  uint32_t eng_posted = 0;
+  int eng_grid = 8;
+  uint64_t eng_idle_ticks = 100000000;  // the kernel's own idle exit: 1 s of wall clock
+  std::atomic<int64_t> eng_last{0};  // steady-clock ns of the last post
+  std::mutex eng_mu;  // posting, starting and stopping the engine
 
   // One copy between a caller's buffer and its staged stripe: `len` bytes at
   // staging row `row` (row * size + off) <-> host + off.
@@ -149,8 +192,12 @@ struct xrs_queue {
     size_t off, len;
   };
 
-  int run(Batch& bt);
+  int launch(Batch& bt);
+  int post(Batch& bt, uint32_t op);
+  void stop_engine();
   void work();
+  void complete();
+  void finish(int i, int err);
   void close_open() {  // (mu held)
     b[open].state = CLOSED;
     b[open].n = b[open].reserved;
@@ -167,7 +214,10 @@ struct xrs_queue {
              const std::vector<int>* has = nullptr, const std::vector<int>* need = nullptr);
 };
 
-int xrs_queue::run(Batch& bt) {
+// Enqueue batch bt on its stream, ending with the write of its sequence
+// number to its host word.  Returns an XRS error if anything failed to
+// enqueue (then no host word write is pending).
+int xrs_queue::launch(Batch& bt) {
   const size_t n = bt.n;
   // Encode: only the data rows go up and only the parity rows come back (one
   // 2-D copy each); ReconstOne: the whole staged stripe up, vect k back;
@@ -185,6 +235,9 @@ int xrs_queue::run(Batch& bt) {
   const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
                                           : rec ? static_cast<size_t>(d + p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
+  bt.engine = false;
+  if (eng_ok && zc && (enc || (!upd && !rec && !rep)))
+    if (post(bt, static_cast<uint32_t>(bt.key)) == 0) return 0;  // (else: launched below)
   uint8_t* base = zc ? bt.host_dev : bt.dev;
   int e = 0;
   if (!zc && hipMemcpy2DAsync(bt.dev + up_off, stripe_bytes, bt.host + up_off, stripe_bytes, up_len,
@@ -213,15 +266,70 @@ int xrs_queue::run(Batch& bt) {
       hipMemcpy2DAsync(bt.host + dn_off, stripe_bytes, bt.dev + dn_off, stripe_bytes, dn_len, n,
                        hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
-  // Completion: spin on the stream (a blocking sync sleeps on an interrupt).
-  hipError_t q;
-  if (block_sync) {
-    q = hipStreamSynchronize(bt.stream);
-  } else {
-    spin_until([&] { return (q = hipStreamQuery(bt.stream)) != hipErrorNotReady; }, spin_ns);
-  }
-  if (q != hipSuccess && !e) e = XRS_ERR_HIP;
+  if (!e && hipStreamWriteValue32(bt.stream, bt.flag_dev, ++bt.launches, 0) != hipSuccess)
+    e = XRS_ERR_HIP;
+  if (e) (void)hipStreamSynchronize(bt.stream);  // nothing of it may still run
   return e;
+}
+
+// Post batch bt (op 0: Encode, 1 + k: ReconstOne(k)) to the resident engine,
+// starting it if needed.  Nonzero: the engine could not be started (the
+// caller launches the batch instead).
+int xrs_queue::post(Batch& bt, uint32_t op) {
+  std::lock_guard<std::mutex> g(eng_mu);
+  const int64_t now = Clock::now().time_since_epoch().count();
+  // (the kernel leaves by itself after 1 s without a descriptor; the host
+  // stops it after kEngineIdleNs, so this only matters if that did not run)
+  if (eng_running && now - eng_last.load() > 500000000 &&
+      hipStreamQuery(eng_stream) == hipSuccess)
+    eng_running = false;
+  if (!eng_running) {
+    __atomic_store_n(&eng_ctl->head, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&eng_ctl->stop, 0u, __ATOMIC_RELAXED);
+    eng_posted = 0;
+    if (xrs::engine_launch(eng_args, eng_ctl_dev, eng_ring_dev, eng_count, eng_grid,
+                           eng_idle_ticks, eng_stream) != 0)
+      return XRS_ERR_HIP;
+    eng_running = true;
+  }
+  xrs::EngineDesc& d = eng_ring[eng_posted % xrs::kEngineRing];
+  d.slot = static_cast<uint32_t>(&bt - b);
+  d.op = op;
+  d.n = static_cast<uint32_t>(bt.n);
+  d.seq = ++bt.launches;
+  d.flag = reinterpret_cast<uint64_t>(bt.flag_dev);
+  __atomic_store_n(&eng_ctl->head, ++eng_posted, __ATOMIC_RELEASE);  // after the descriptor
+  eng_last.store(now);
+  bt.engine = true;
+  return 0;
+}
+
+// Stop the resident engine once everything posted is done (it leaves its loop
+// when it has caught up with head and sees stop).
+void xrs_queue::stop_engine() {
+  std::lock_guard<std::mutex> g(eng_mu);
+  if (!eng_running) return;
+  __atomic_store_n(&eng_ctl->stop, 1u, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(eng_stream);
+  __atomic_store_n(&eng_ctl->stop, 0u, __ATOMIC_RELAXED);
+  eng_running = false;
+}
+
+// Batch i's results are in staging (or it failed): release its callers.
+void xrs_queue::finish(int i, int err) {
+  Batch& bt = b[i];
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    bt.err = err;
+    bt.state = DONE;
+    --in_flight;
+    ++st_batches;
+    st_stripes += bt.n;
+    st_run_ns += ns_since(bt.launched);
+    cv_work.notify_one();  // a launcher may wait for in_flight < max_inflight
+  }
+  bt.done.fetch_add(1, std::memory_order_release);
+  futex_wake_all(&bt.done);
 }
 
 void xrs_queue::work() {
@@ -236,13 +344,16 @@ void xrs_queue::work() {
       if (bt.state == OPEN || bt.state == CLOSED) pending = true;
       if (bt.state == CLOSED) pick = i;
       if (bt.state == OPEN && bt.reserved > 0) {
-        bool go = !timer || stop;  // (stopping: drain, every caller already in gets its result)
-        if (!go) {
+        // (stopping: drain, every caller already in gets its result)
+        bool go = stop;
+        if (!go && !timer) {
+          go = in_flight < max_inflight;
+        } else if (!go) {
           // timer: a small batch runs at once when nothing is in flight;
           // otherwise, and for large stripes (PCIe-bound, where bigger
           // batches measured faster), it grows until max_wait has passed.
           const auto due = bt.opened + max_wait;
-          go = (running == 0 && bt.reserved * stripe_bytes <= zc_max) || Clock::now() >= due;
+          go = (in_flight == 0 && bt.reserved * stripe_bytes <= zc_max) || Clock::now() >= due;
           if (!go) next = std::min(next, due);
         }
         if (go) {
@@ -253,34 +364,87 @@ void xrs_queue::work() {
     }
     if (pick < 0) {
       if (stop && !pending) break;
+      if (eng_running.load() && in_flight == 0 &&
+          Clock::now().time_since_epoch().count() - eng_last.load() > kEngineIdleNs) {
+        lk.unlock();
+        stop_engine();
+        lk.lock();
+        continue;
+      }
       cv_work.wait_until(lk, next);
       continue;
     }
     Batch& bt = b[pick];
-    bt.state = RUNNING;
-    ++running;
+    bt.state = LAUNCHING;
+    ++in_flight;
     const size_t n = bt.n;
     lk.unlock();
     // the batch's callers are still copying in (a few us at 4 KiB)
     spin_until([&] { return bt.filled.load(std::memory_order_acquire) == n; }, spin_ns);
-    const auto t0 = Clock::now();
-    const uint64_t waited =
-        std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - bt.opened).count();
-    const int e = run(bt);
-    const uint64_t ran =
-        std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+    bt.launched = Clock::now();
+    const uint64_t waited = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                bt.launched - bt.opened).count();
+    const int e = launch(bt);
     lk.lock();
-    bt.err = e;
-    bt.state = DONE;
-    --running;
-    ++st_batches;
-    st_stripes += n;
-    st_run_ns += ran;
     st_wait_ns += waited;
-    lk.unlock();
-    bt.done.fetch_add(1, std::memory_order_release);
-    futex_wake_all(&bt.done);
-    lk.lock();
+    if (e) {
+      lk.unlock();
+      finish(pick, e);
+      lk.lock();
+      continue;
+    }
+    bt.state = INFLIGHT;
+    inflight_bits.fetch_or(1u << pick, std::memory_order_release);
+    cv_comp.notify_one();
+  }
+}
+
+void xrs_queue::complete() {
+  if (device >= 0) (void)hipSetDevice(device);
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv_comp.wait(lk, [&] {
+        return inflight_bits.load(std::memory_order_acquire) != 0 || (comp_stop && in_flight == 0);
+      });
+      if (inflight_bits.load(std::memory_order_acquire) == 0) return;  // stopping, drained
+    }
+    // Spin on the host words of every batch in flight (new launches join the
+    // mask as they happen) until none is left.  A failed stream never writes
+    // its word, so a batch still waiting after kStuckNs gets hipStreamQuery
+    // checks (which are not free: spinning on hipStreamQuery saw an empty
+    // kernel done 5-9 us later than its host word, r03_queue_latency_probe).
+    auto idle = Clock::now();
+    for (uint32_t it = 1;; ++it) {
+      uint32_t bits = inflight_bits.load(std::memory_order_acquire);
+      if (!bits) break;
+      bool any = false;
+      const bool poll = (it & 1023) == 0;
+      for (uint32_t m = bits; m; m &= m - 1) {
+        const int i = __builtin_ctz(m);
+        Batch& bt = b[i];
+        int err = -1;
+        if (*bt.flag == bt.launches) {
+          err = 0;
+        } else if (poll && ns_since(bt.launched) > kStuckNs) {
+          const hipError_t q = hipStreamQuery(bt.engine ? eng_stream : bt.stream);
+          if (q == hipSuccess) err = *bt.flag == bt.launches ? 0 : XRS_ERR_HIP;
+          else if (q != hipErrorNotReady) err = XRS_ERR_HIP;
+        }
+        if (err < 0) continue;
+        std::atomic_thread_fence(std::memory_order_acquire);  // staging after the word
+        inflight_bits.fetch_and(~(1u << i), std::memory_order_acq_rel);
+        finish(i, err);
+        any = true;
+      }
+      if (any) {
+        idle = Clock::now();
+      } else if (ns_since(idle) > comp_spin_ns) {
+        std::this_thread::yield();
+      } else {
+        _mm_pause();
+      }
+    }
   }
 }
 
@@ -304,7 +468,7 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       }
       if (open >= 0 && b[open].key == key && b[open].reserved < max_batch && same_pattern(b[open]))
         break;
-      if (open >= 0) close_open();  // different op or full: the worker runs it
+      if (open >= 0) close_open();  // different op or full: a launcher runs it
       int f = -1;
       for (int i = 0; i < n_batches && f < 0; ++i)
         if (b[i].state == FREE) f = i;
@@ -325,7 +489,7 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
         nb.pat_need = *need;
       }
       open = f;
-      if (!timer) cv_work.notify_one();  // a free worker takes it at once
+      if (!timer) cv_work.notify_one();  // a free launcher takes it at once
     }
     bp = &b[open];
     slot = bp->reserved++;
@@ -339,7 +503,7 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
     std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
   bt.filled.fetch_add(1, std::memory_order_release);
   if (timer) {
-    // the timer policy's worker may be asleep on a batch that is now staged
+    // the timer policy's launcher may be asleep on a batch that is now staged
     std::lock_guard<std::mutex> lk(mu);
     cv_work.notify_one();
   }
@@ -355,6 +519,27 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   }
   leave();
   return err;
+}
+
+// The resident engine's stream must own its hardware queue: streams beyond
+// GPU_MAX_HW_QUEUES share queues, and a kernel queued behind the resident one
+// on a shared queue waits until it leaves (tools/persist_probe.hip `block`:
+// 4 of 8 other streams stalled for an ordinary stream, none for a CU-masked or
+// a greatest-priority one, profiles/r03_persist_probe.log).  A CU-masked
+// stream (every CU) gets a queue of its own; the greatest-priority stream is
+// the fallback.
+static hipError_t engine_stream(hipStream_t* s) {
+  hipDeviceProp_t prop;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+      prop.multiProcessorCount > 0) {
+    std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, ~0u);
+    if (hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess)
+      return hipSuccess;
+  }
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return hipErrorInvalidValue;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
 }
 
 extern "C" {
@@ -379,21 +564,31 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   q->max_wait = std::chrono::microseconds(max_wait_us);
   const char* zv = std::getenv("XRS_QUEUE_ZC_MAX");
   q->zc_max = (zv && *zv) ? static_cast<size_t>(std::strtoull(zv, nullptr, 0)) : (4u << 20);
-  const char* wv = std::getenv("XRS_QUEUE_WORKERS");
-  if (wv && *wv) q->n_workers = std::max(1, std::min(kMaxWorkers, std::atoi(wv)));
-  q->n_batches = q->n_workers + 2;
+  auto env_int = [](const char* v, int lo, int hi, int def) {
+    const char* e = std::getenv(v);
+    return (e && *e) ? std::max(lo, std::min(hi, std::atoi(e))) : def;
+  };
+  q->n_workers = env_int("XRS_QUEUE_WORKERS", 1, kMaxWorkers, 1);
+  q->max_inflight = env_int("XRS_QUEUE_INFLIGHT", 1, kBatches - 1, 4);
+  q->n_batches = env_int("XRS_QUEUE_BATCHES", 2, kBatches, std::min(kBatches, q->max_inflight + 2));
   const char* pv = std::getenv("XRS_QUEUE_POLICY");
   q->timer = pv && std::strcmp(pv, "timer") == 0;
-  const char* sv = std::getenv("XRS_QUEUE_SYNC");
-  q->block_sync = sv && std::strcmp(sv, "block") == 0;
   const char* nv = std::getenv("XRS_QUEUE_SPIN_NS");
   if (nv && *nv) q->spin_ns = std::strtoull(nv, nullptr, 0);
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
   int e = XRS_OK;
-  for (int i = 0; i < q->n_batches; ++i) {
+  void* fp = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&q->flags), kBatches * kFlagStride * sizeof(uint32_t),
+                    hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(&fp, q->flags, 0) != hipSuccess)
+    e = XRS_ERR_HIP;
+  for (int i = 0; i < q->n_batches && !e; ++i) {
     Batch& bt = q->b[i];
+    bt.flag = q->flags + i * kFlagStride;
+    *bt.flag = 0;
+    bt.flag_dev = static_cast<uint32_t*>(fp) + i * kFlagStride;
     if (hipHostMalloc(&bt.host, q->max_batch * q->stripe_bytes, hipHostMallocMapped) != hipSuccess ||
         hipMalloc(&bt.dev, q->max_batch * q->stripe_bytes) != hipSuccess ||
         hipStreamCreateWithFlags(&bt.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -409,11 +604,54 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     }
     bt.rows_dev = static_cast<int32_t*>(dp);
   }
+  const char* ev = std::getenv("XRS_QUEUE_ENGINE");
+  if (!e && (ev && ev[0] == '1') && q->d == 12 && q->p == 4 && size % 32 == 0 &&
+      q->zc_max >= q->stripe_bytes) {
+    // one argument block per staging slot, from the plans the launched path
+    // would run on that slot (captured, not launched)
+    std::vector<xrs::PairPlan> enc_all, enc;
+    std::vector<xrs::RowsPlan> rec_all, rec;
+    std::vector<int> cnt;
+    bool ok = true;
+    for (int i = 0; i < q->n_batches && ok; ++i) {
+      ok = q->b[i].host_dev &&
+           xrs_detail::capture_plans(codec, q->b[i].host_dev, size, q->stripe_bytes, &enc, &rec,
+                                     &cnt) == XRS_OK &&
+           enc.size() == 1 && rec.size() == static_cast<size_t>(q->d);
+      for (int c : cnt) ok = ok && c == 1;
+      if (ok) {
+        enc_all.push_back(enc[0]);
+        rec_all.insert(rec_all.end(), rec.begin(), rec.end());
+      }
+    }
+    void* cp = nullptr;
+    void* rp = nullptr;
+    int khz = 0;
+    if (ok && xrs::engine_prepare(enc_all.data(), rec_all.data(), q->n_batches, q->d, &q->eng_args) == 0 &&
+        hipHostMalloc(reinterpret_cast<void**>(&q->eng_ctl), sizeof(xrs::EngineCtl), hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer(&cp, q->eng_ctl, 0) == hipSuccess &&
+        hipHostMalloc(reinterpret_cast<void**>(&q->eng_ring), sizeof(xrs::EngineDesc) * xrs::kEngineRing,
+                      hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer(&rp, q->eng_ring, 0) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&q->eng_count), sizeof(uint32_t) * xrs::kEngineRing) == hipSuccess &&
+        engine_stream(&q->eng_stream) == hipSuccess) {
+      std::memset(q->eng_ctl, 0, sizeof(xrs::EngineCtl));
+      std::memset(q->eng_ring, 0, sizeof(xrs::EngineDesc) * xrs::kEngineRing);
+      q->eng_ctl_dev = static_cast<xrs::EngineCtl*>(cp);
+      q->eng_ring_dev = static_cast<xrs::EngineDesc*>(rp);
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+        q->eng_idle_ticks = static_cast<uint64_t>(khz) * 1000;  // 1 s
+      q->eng_grid = env_int("XRS_QUEUE_ENGINE_GRID", 1, 64, 8);
+      q->eng_ok = true;
+    }
+    // (without the engine every batch is launched: nothing else changes)
+  }
   if (prev >= 0) (void)hipSetDevice(prev);
   if (e) {
     xrs_queue_free(q);
     return e;
   }
+  q->completer = std::thread([q] { q->complete(); });
   for (int i = 0; i < q->n_workers; ++i) q->worker[i] = std::thread([q] { q->work(); });
   *out = q;
   return XRS_OK;
@@ -423,7 +661,8 @@ void xrs_queue_free(xrs_queue* q) {
   if (!q) return;
   {
     // New calls fail from here on; calls already holding a slot complete
-    // (the workers drain every open batch before they exit), and the queue
+    // (the launchers drain every open batch before they exit, the completion
+    // thread every batch in flight), and the queue
     // is torn down only after the last caller has left submit().
     std::unique_lock<std::mutex> lk(q->mu);
     q->stop = true;
@@ -433,15 +672,28 @@ void xrs_queue_free(xrs_queue* q) {
   }
   for (auto& w : q->worker)
     if (w.joinable()) w.join();
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->comp_stop = true;
+    q->cv_comp.notify_all();
+  }
+  if (q->completer.joinable()) q->completer.join();
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (q->device >= 0) (void)hipSetDevice(q->device);
+  q->stop_engine();
+  if (q->eng_stream) (void)hipStreamDestroy(q->eng_stream);
+  xrs::engine_release(q->eng_args);
+  if (q->eng_count) (void)hipFree(q->eng_count);
+  if (q->eng_ctl) (void)hipHostFree(q->eng_ctl);
+  if (q->eng_ring) (void)hipHostFree(q->eng_ring);
   for (Batch& bt : q->b) {
     if (bt.stream) (void)hipStreamDestroy(bt.stream);
     if (bt.dev) (void)hipFree(bt.dev);
     if (bt.host) (void)hipHostFree(bt.host);
     if (bt.rows) (void)hipHostFree(bt.rows);
   }
+  if (q->flags) (void)hipHostFree(q->flags);
   if (prev >= 0) (void)hipSetDevice(prev);
   delete q;
 }
@@ -587,6 +839,43 @@ int xrs_queue_stats(xrs_queue* q, uint64_t out[4]) {
   out[2] = q->st_run_ns;
   out[3] = q->st_wait_ns;
   return XRS_OK;
+}
+
+size_t xrs_queue_dump(xrs_queue* q, char* buf, size_t cap) {
+  if (!q) return 0;
+  std::unique_lock<std::mutex> lk(q->mu, std::defer_lock);
+  for (int i = 0; i < 100 && !lk.try_lock(); ++i) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  static const char* names[] = {"FREE", "OPEN", "CLOSED", "LAUNCHING", "INFLIGHT", "DONE"};
+  std::string out;
+  char line[256];
+  std::snprintf(line, sizeof line, "lock %s open %d in_flight %d bits 0x%x active %d stop %d\n",
+                lk.owns_lock() ? "taken" : "BUSY", q->open, q->in_flight, q->inflight_bits.load(),
+                q->active.load(), q->stop ? 1 : 0);
+  out += line;
+  if (q->eng_ok) {
+    std::snprintf(line, sizeof line, "engine running %d posted %u head %u stop %u seen %u polls %u\n",
+                  q->eng_running.load() ? 1 : 0, q->eng_posted,
+                  __atomic_load_n(&q->eng_ctl->head, __ATOMIC_RELAXED),
+                  __atomic_load_n(&q->eng_ctl->stop, __ATOMIC_RELAXED),
+                  __atomic_load_n(&q->eng_ctl->seen, __ATOMIC_RELAXED),
+                  __atomic_load_n(&q->eng_ctl->polls, __ATOMIC_RELAXED));
+    out += line;
+  }
+  for (int i = 0; i < q->n_batches; ++i) {
+    const Batch& bt = q->b[i];
+    std::snprintf(line, sizeof line,
+                  "batch %d %s key %d reserved %zu n %zu filled %u released %u done %u launches %u "
+                  "flag %u err %d engine %d\n",
+                  i, names[bt.state], bt.key, bt.reserved, bt.n, bt.filled.load(), bt.released.load(),
+                  bt.done.load(), bt.launches, bt.flag ? *bt.flag : 0u, bt.err, bt.engine ? 1 : 0);
+    out += line;
+  }
+  if (buf && cap) {
+    const size_t n = std::min(out.size(), cap - 1);
+    std::memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
+  return out.size();
 }
 
 }  // extern "C"

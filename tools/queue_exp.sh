@@ -1,7 +1,6 @@
 #!/bin/bash
 # Batching-queue experiments (tools/sync_bench): the queue's GPU tests, then
-# CONFIGS of policy:launchers:inflight[:engine], THREADS callers, SIZES vects
-# (engine 0: XRS_QUEUE_ENGINE=0, every batch launched).
+# CONFIGS of policy:launchers:inflight, THREADS callers, SIZES vects.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -10,14 +9,14 @@ if [ "${QTEST:-1}" = 1 ]; then
     --timeout 120 --timeout-method thread > gpurun_out/q_pytest.log 2>&1
   rc=$?; tail -3 gpurun_out/q_pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
-CONFIGS=${CONFIGS:-"free:1:2 free:1:3 free:1:4 free:2:3 free:2:6"}
+CONFIGS=${CONFIGS:-"free:1:4 free:1:6 free:2:4 timer:1:4"}
 THREADS=${THREADS:-"1 8 16 32 48"}
 SIZES=${SIZES:-4096}
 for size in $SIZES; do
 for cfg in $CONFIGS; do
-  IFS=: read -r pol w inf eng <<< "$cfg"
-  echo "size=$size policy=$pol launchers=$w inflight=$inf engine=${eng:-1}"
-  XRS_QUEUE_POLICY=$pol XRS_QUEUE_WORKERS=$w XRS_QUEUE_INFLIGHT=$inf XRS_QUEUE_ENGINE=${eng:-1} \
+  IFS=: read -r pol w inf <<< "$cfg"
+  echo "size=$size policy=$pol launchers=$w inflight=$inf"
+  XRS_QUEUE_POLICY=$pol XRS_QUEUE_WORKERS=$w XRS_QUEUE_INFLIGHT=$inf \
     timeout -k 10 90 tools/sync_bench $size queue 50 $THREADS
   rc=$?
   echo "rc=$rc"

@@ -71,11 +71,6 @@ struct XorSrc {
   std::vector<int> outs;  // outputs this row is XORed into
 };
 
-// Plan capture (the batching queue's engine): while set on this thread,
-// run_pair / run_rows append their plans here instead of launching them.
-thread_local std::vector<xrs::PairPlan>* g_cap_pair = nullptr;
-thread_local std::vector<xrs::RowsPlan>* g_cap_rows = nullptr;
-
 // Pair plans: outputs in groups of kMaxOut, sources in chunks of kMaxSrc; the
 // first chunk of each group writes (or accumulates if acc), later chunks add.
 int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, bool acc,
@@ -109,7 +104,7 @@ int run_pair(const std::vector<RowRef>& dst, const std::vector<MulSrc>& src, boo
         for (int r = 0; r < P; ++r) plan.tab[c][r] = gf.tab(s.coef[g0 + r]);
         plan.pb[c] = (s.pb >= g0 && s.pb < g0 + P) ? static_cast<int8_t>(s.pb - g0) : -1;
       }
-      const int e = g_cap_pair ? (g_cap_pair->push_back(plan), 0) : xrs::launch_pair(plan, stream);
+      const int e = xrs::launch_pair(plan, stream);
       if (e != 0) return XRS_ERR_HIP;
       c0 += C;
     } while (c0 < ns);
@@ -156,7 +151,7 @@ int run_rows(const std::vector<RowRef>& dst, const std::vector<MulSrc>& msrc,
         plan.xsrc[x] = xs[x0 + x].first;
         plan.xmask[x] = xs[x0 + x].second;
       }
-      const int e = g_cap_rows ? (g_cap_rows->push_back(plan), 0) : xrs::launch_rows(plan, stream);
+      const int e = xrs::launch_rows(plan, stream);
       if (e != 0) return XRS_ERR_HIP;
       m0 += NM;
       x0 += NX;
@@ -874,29 +869,6 @@ int reconst_one_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard
 }
 int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi) {
   return need_vects(x, k, a_need, bi);
-}
-// The plans Encode and ReconstOne(k) for every k would launch on a batch at
-// `base` (shard stride = size), captured instead of launched: enc gets
-// Encode's plans, rec the concatenated ReconstOne plans, rec_count[k] how many
-// ReconstOne(k) made.
-int capture_plans(const xrs_codec* x, uint8_t* base, size_t size, size_t stripe_stride,
-                  std::vector<xrs::PairPlan>* enc, std::vector<xrs::RowsPlan>* rec,
-                  std::vector<int>* rec_count) {
-  enc->clear();
-  rec->clear();
-  rec_count->clear();
-  const Layout L{base, size, stripe_stride};
-  g_cap_pair = enc;
-  int e = encode_impl(x, L, size, 1, nullptr);
-  g_cap_pair = nullptr;
-  for (int k = 0; k < x->d && !e; ++k) {
-    const size_t before = rec->size();
-    g_cap_rows = rec;
-    e = reconst_one_impl(x, L, size, 1, k, nullptr);
-    g_cap_rows = nullptr;
-    rec_count->push_back(static_cast<int>(rec->size() - before));
-  }
-  return e;
 }
 int codec_device(const xrs_codec* x) { return x->device; }
 int codec_d(const xrs_codec* x) { return x->d; }

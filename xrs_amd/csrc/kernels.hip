@@ -36,9 +36,8 @@
 #include "xrs_plan.h"
 
 // Build parts: the Makefile compiles this file once per XRS_PART (1: launch
-// trace + pair kernels, 2: staged, 3: update_rows, 4: rows, 5: the batching
-// queue's resident engine), so the gfx950 code generation of the kernel
-// families runs in parallel.  Without
+// trace + pair kernels, 2: staged, 3: update_rows, 4: rows), so the gfx950
+// code generation of the kernel families runs in parallel.  Without
 // XRS_PART (tools/, the host-sanitizer test build) one unit holds everything.
 #ifndef XRS_PART
 #define XRS_PART 0
@@ -240,89 +239,6 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
 // plain order (launch_pair_t).  It also gives that launch, the bench's
 // dominant one, its own name in rocprofv3 --stats (the 4 KiB Encode runs the
 // same <4, 12, false, true, 128> shape in the XCD order).
-// One lane's work of pair_kernel (below) for lane index gid, reading `a`
-// through a reference: the batching queue's resident engine (part 5) keeps
-// its arguments in device memory.  The launched kernel keeps its own copy of
-// this code: routing it through this body raised the 12+4 Encode from 170 to
-// 286 VGPRs (AGPRs in use, one wave per SIMD; tests/test_kernel_resources.py).
-template <int P, int C, bool ACC, bool VEC>
-__device__ __forceinline__ void pair_body(const PairArgs<P, C, VEC>& a, uint64_t gid) {
-  constexpr int W = VEC ? 4 : 1;
-  const uint64_t stripe = gid / a.chunks;
-  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
-  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
-
-  uint32_t acc_a[P][W], acc_b[P][W];
-  if constexpr (ACC) {
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      const uint64_t d = row_addr(a.dst[r], stripe, off);
-      ld<VEC>(acc_a[r], d, nb);
-      ld<VEC>(acc_b[r], d + a.half, nb);
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < P; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc_a[r][w] = acc_b[r][w] = 0u;
-  }
-
-  if constexpr (C != kDyn) {
-    // Compile-time source count: every load issued up front.
-    uint32_t xa[C][W], xb[C][W];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const uint64_t s = row_addr(a.src[c], stripe, off);
-      ld<VEC>(xa[c], s, nb);
-      ld<VEC>(xb[c], s + a.half, nb);
-    }
-#pragma unroll
-    for (int c = 0; c + 1 < C; c += 2)
-      pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
-    if constexpr (C & 1) pair_mac1<P, W>(acc_a, acc_b, a.tab[C - 1], xa[C - 1], xb[C - 1]);
-    if constexpr (!ACC) {
-      // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
-      // c rides on parity 1 + c % (P-1).  Compile-time source counts are only
-      // launched for a whole Encode (PairPlan::encode_xs).
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
-    } else {
-#pragma unroll
-      for (int c = 0; c < C; ++c) piggyback<P, W>(acc_b, a.pbmask, c, xa[c]);
-    }
-  } else {
-    // Runtime source count: groups of kGrp sources, each group's loads issued
-    // together (wave-uniform guards keep the register indexes static).
-    constexpr int kGrp = 6;
-    for (int c0 = 0; c0 < a.n_src; c0 += kGrp) {
-      uint32_t xa[kGrp][W], xb[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (c0 + g < a.n_src) {
-          const uint64_t s = row_addr(a.src[c0 + g], stripe, off);
-          ld<VEC>(xa[g], s, nb);
-          ld<VEC>(xb[g], s + a.half, nb);
-        }
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (c0 + g < a.n_src) {
-          pair_mac1<P, W>(acc_a, acc_b, a.tab[c0 + g], xa[g], xb[g]);
-          piggyback<P, W>(acc_b, a.pbmask, c0 + g, xa[g]);
-        }
-    }
-  }
-
-#pragma unroll
-  for (int r = 0; r < P; ++r) {
-    const uint64_t d = row_addr(a.dst[r], stripe, off);
-    st<VEC>(acc_a[r], d, nb);
-    st<VEC>(acc_b[r], d + a.half, nb);
-  }
-}
-
 template <int P, int C, bool ACC, bool VEC, int BS = kBlock, bool PLAIN = false>
 __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
   constexpr int W = VEC ? 4 : 1;
@@ -460,86 +376,6 @@ __device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, c
 #pragma unroll
     for (int w = 0; w < W; ++w) acc[r][w] = xor_masked(acc[r][w], x[w], m);
   }
-}
-
-// One lane's work of rows_kernel (below) through a reference, for the
-// resident engine (as pair_body).
-template <int R, int NM, int NX, bool ACC, bool VEC>
-__device__ __forceinline__ void rows_body(const RowsArgs<R, NM, NX, VEC>& a, uint64_t gid) {
-  constexpr int W = VEC ? 4 : 1;
-  const uint64_t stripe = gid / a.chunks;
-  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
-  const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
-
-  uint32_t acc[R][W];
-  if constexpr (ACC) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) ld<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-  }
-
-  if constexpr (NM != kDyn && NX != kDyn) {
-    uint32_t xm[NM > 0 ? NM : 1][W], xx[NX > 0 ? NX : 1][W];
-    // Raised priority while this wave issues its loads, so fresh waves get
-    // their requests out ahead of waves that are computing (measured +1.7%
-    // on ReconstOne 1 MiB; tools/kbench.hip "rw prio").
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < NM; ++m) ld<VEC>(xm[m], row_addr(a.msrc[m], stripe, off), nb);
-#pragma unroll
-    for (int x = 0; x < NX; ++x) ld<VEC>(xx[x], row_addr(a.xsrc[x], stripe, off), nb);
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int m = 0; m + 1 < NM; m += 2) rows_mac2<R, W>(acc, a.tab[m], a.tab[m + 1], xm[m], xm[m + 1]);
-    if constexpr (NM & 1) rows_mac1<R, W>(acc, a.tab[NM - 1], xm[NM - 1]);
-#pragma unroll
-    for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
-  } else if (a.grouped) {
-    // Runtime counts, small grid (latency-bound): groups of kGrp rows, each
-    // group's loads issued together, so a launch pays ceil(rows / kGrp)
-    // memory round trips instead of one per row.
-    constexpr int kGrp = 8;
-    for (int m0 = 0; m0 < a.nm; m0 += kGrp) {
-      uint32_t v[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (m0 + g < a.nm) ld<VEC>(v[g], row_addr(a.msrc[m0 + g], stripe, off), nb);
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (m0 + g < a.nm) rows_mac1<R, W>(acc, a.tab[m0 + g], v[g]);
-    }
-    for (int x0 = 0; x0 < a.nx; x0 += kGrp) {
-      uint32_t v[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (x0 + g < a.nx) ld<VEC>(v[g], row_addr(a.xsrc[x0 + g], stripe, off), nb);
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (x0 + g < a.nx) rows_xor<R, W>(acc, a.xmask[x0 + g], v[g]);
-    }
-  } else {
-    // Runtime counts, large grid: one row at a time (measured: grouping 8
-    // loads per wave cost 0-2% at 4 KiB and 2-7% at 1 MiB over seven (d, p)
-    // in the XCD order; profiles/r01_others_rows_grouped{0,1}.log).
-    for (int m = 0; m < a.nm; ++m) {
-      uint32_t v[W];
-      ld<VEC>(v, row_addr(a.msrc[m], stripe, off), nb);
-      rows_mac1<R, W>(acc, a.tab[m], v);
-    }
-    for (int x = 0; x < a.nx; ++x) {
-      uint32_t v[W];
-      ld<VEC>(v, row_addr(a.xsrc[x], stripe, off), nb);
-      rows_xor<R, W>(acc, a.xmask[x], v);
-    }
-  }
-
-#pragma unroll
-  for (int r = 0; r < R; ++r) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
 }
 
 template <int R, int NM, int NX, bool ACC, bool VEC, int BS = kBlock>
@@ -2109,168 +1945,5 @@ int launch_rows(const RowsPlan& p0, void* stream) {
 }
 
 #endif  // XRS_HAS_PART(4)
-
-#if XRS_HAS_PART(5)
-// ============================================================ queue engine
-// The batching queue's resident kernel (queue.cpp): G workgroups stay on the
-// GPU and poll a descriptor ring in pinned host memory, so a small batch of
-// per-stripe calls costs no launch.  Descriptor q names a staging slot, an op
-// (Encode, or ReconstOne(k)) and a stripe count; every workgroup takes its
-// share of the batch's lanes (lane i -> workgroup (i / BS) mod G) through the
-// same pair / rows bodies as the launched kernels, with arguments prepared
-// per slot in device memory.  After its share a workgroup waits for its
-// stores, then counts itself done on the ring entry's device counter; the
-// G-th writes the descriptor's sequence number to the batch's host word.  Every wave leaves when the host sets `stop` with nothing posted, or
-// after `idle_ticks` of the 100 MHz wall clock without a descriptor, so the
-// grid always drains.  Measured round trip for 8 x 4 KiB stripes (12+4
-// Encode traffic): 14.8 us resident (G = 8) against 23 us launched
-// (tools/persist_probe.hip, profiles/r03_persist_probe.log).
-namespace {
-
-constexpr int kEngineBlock = 256;
-
-template <int P, int C, int NM, int NX>
-struct EngineSlot {
-  PairArgs<P, C, true> enc;                 // Encode of the slot's staging
-  RowsArgs<2, NM, NX, true> rec[kMaxSrc];   // ReconstOne(k), k < d
-};
-
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-template <int P, int C, int NM, int NX>
-__global__ __launch_bounds__(kEngineBlock) void queue_engine(EngineCtl* ctl, const EngineDesc* ring,
-                                                             const EngineSlot<P, C, NM, NX>* slots,
-                                                             uint32_t* count, uint64_t idle_ticks) {
-  __shared__ uint32_t sh[2];
-  const uint32_t G = gridDim.x;
-  uint32_t seen = 0;  // descriptors done by this workgroup
-  uint32_t polls = 0;
-  uint64_t t_idle = wall_clock64();
-  for (;;) {
-    if (threadIdx.x == 0) {
-      sh[0] = __hip_atomic_load(&ctl->head, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      sh[1] = ld_sys(&ctl->stop);
-    }
-    __syncthreads();
-    const uint32_t head = sh[0], stop = sh[1];
-    __syncthreads();
-    if (head == seen) {
-      if (stop || wall_clock64() - t_idle > idle_ticks) break;
-      if (blockIdx.x == 0 && threadIdx.x == 0 && (++polls & 1023) == 0)
-        __hip_atomic_store(&ctl->polls, polls >> 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    // Every descriptor posted so far (up to 8) in one sweep: the completion
-    // handshake below is paid once per sweep, not once per batch.
-    const uint32_t end = head - seen > 8 ? seen + 8 : head;
-    const uint64_t stride = static_cast<uint64_t>(G) * kEngineBlock;
-    for (uint32_t q = seen; q != end; ++q) {
-      // (vector atomic loads: host memory is never read through the scalar cache)
-      const uint64_t* d = reinterpret_cast<const uint64_t*>(&ring[q % kEngineRing]);
-      const uint64_t w0 = ld_sys64(d), w1 = ld_sys64(d + 1);
-      const uint32_t slot = static_cast<uint32_t>(w0), op = static_cast<uint32_t>(w0 >> 32);
-      const uint32_t n = static_cast<uint32_t>(w1);
-      const EngineSlot<P, C, NM, NX>& S = slots[slot];
-      if (op == 0) {
-        const uint64_t items = static_cast<uint64_t>(n) * S.enc.chunks;
-        for (uint64_t i = blockIdx.x * kEngineBlock + threadIdx.x; i < items; i += stride)
-          pair_body<P, C, false, true>(S.enc, i);
-      } else {
-        const RowsArgs<2, NM, NX, true>& R = S.rec[op - 1];
-        const uint64_t items = static_cast<uint64_t>(n) * R.chunks;
-        for (uint64_t i = blockIdx.x * kEngineBlock + threadIdx.x; i < items; i += stride)
-          rows_body<2, NM, NX, false, true>(R, i);
-      }
-    }
-    // Every wave's stores acknowledged (vmcnt counts stores on gfx9; the
-    // staging is fine-grained host memory, written past the L2), then the
-    // workgroup counts itself done on each descriptor's counter; the G-th
-    // arrival writes the batch's sequence number with a system-scope release.
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (uint32_t q = seen; q != end; ++q) {
-        // one counter per ring entry: workgroups run through the ring at
-        // their own pace.  The last arrival resets it (the entry is reused
-        // only after the host saw this batch done).
-        uint32_t* c = &count[q % kEngineRing];
-        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 == G) {
-          const uint64_t* d = reinterpret_cast<const uint64_t*>(&ring[q % kEngineRing]);
-          const uint64_t w1 = ld_sys64(d + 1), w2 = ld_sys64(d + 2);
-          __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(reinterpret_cast<uint32_t*>(w2), static_cast<uint32_t>(w1 >> 32),
-                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-      if (blockIdx.x == 0)
-        __hip_atomic_store(&ctl->seen, end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    seen = end;
-    t_idle = wall_clock64();
-  }
-}
-
-using Engine12p4 = EngineSlot<4, 12, 12, 4>;
-
-}  // namespace
-
-int engine_prepare(const PairPlan* enc, const RowsPlan* rec, int n_slots, int d, void** dev_args) {
-  *dev_args = nullptr;
-  if (n_slots < 1 || d != 12) return kEngineUnsupported;
-  std::vector<Engine12p4> h(n_slots);
-  for (int i = 0; i < n_slots; ++i) {
-    const PairPlan& e = enc[i];
-    if (e.P != 4 || e.C != 12 || e.acc || !e.encode_xs || e.half % 16) return kEngineUnsupported;
-    PairPlan pe = e;
-    pe.off0 = 0;
-    pe.end = e.half;
-    pe.overlap = false;
-    pe.n_stripes = 0;
-    fill_pair_args(h[i].enc, pe);
-    for (int k = 0; k < d; ++k) {
-      const RowsPlan& r = rec[i * d + k];
-      if (r.R != 2 || r.NM != 12 || r.NX != 4 || r.acc || r.len % 16) return kEngineUnsupported;
-      RowsPlan pr = r;
-      pr.off0 = 0;
-      pr.end = r.len;
-      pr.overlap = false;
-      pr.n_stripes = 0;
-      fill_rows_args(h[i].rec[k], pr);
-    }
-  }
-  void* p = nullptr;
-  if (hipMalloc(&p, sizeof(Engine12p4) * n_slots) != hipSuccess) return static_cast<int>(hipErrorOutOfMemory);
-  if (hipMemcpy(p, h.data(), sizeof(Engine12p4) * n_slots, hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(p);
-    return static_cast<int>(hipErrorInvalidValue);
-  }
-  *dev_args = p;
-  return 0;
-}
-
-int engine_launch(const void* dev_args, EngineCtl* ctl, const EngineDesc* ring, uint32_t* count,
-                  int grid, uint64_t idle_ticks, void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (grid < 1 || grid > 64) return static_cast<int>(hipErrorInvalidValue);
-  if (hipMemsetAsync(count, 0, sizeof(uint32_t) * kEngineRing, s) != hipSuccess)
-    return static_cast<int>(hipErrorInvalidValue);
-  (void)hipGetLastError();
-  XRS_LAUNCH((queue_engine<4, 12, 12, 4>), dim3(grid), dim3(kEngineBlock), s, ctl, ring,
-             static_cast<const Engine12p4*>(dev_args), count, idle_ticks);
-  return static_cast<int>(hipGetLastError());
-}
-
-void engine_release(void* dev_args) {
-  if (dev_args) (void)hipFree(dev_args);
-}
-#endif  // XRS_HAS_PART(5)
 
 }  // namespace xrs

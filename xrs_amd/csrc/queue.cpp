@@ -57,7 +57,6 @@
 #include <vector>
 
 #include "xrs_hip.h"
-#include "xrs_plan.h"
 
 namespace xrs_detail {
 int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
@@ -68,9 +67,6 @@ int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi);
 int codec_device(const xrs_codec* x);
 int codec_d(const xrs_codec* x);
 int codec_p(const xrs_codec* x);
-int capture_plans(const xrs_codec* x, uint8_t* base, size_t size, size_t stripe_stride,
-                  std::vector<xrs::PairPlan>* enc, std::vector<xrs::RowsPlan>* rec,
-                  std::vector<int>* rec_count);
 }  // namespace xrs_detail
 
 using Clock = std::chrono::steady_clock;
@@ -82,7 +78,6 @@ constexpr int kBatches = 16;     // staging buffers: XRS_QUEUE_BATCHES, default 
 constexpr int kFlagStride = 16;  // uint32 words between batches' host words (64 B)
 constexpr size_t kMaxBatchBytes = 64u << 20;
 constexpr uint64_t kStuckNs = 20000000;  // in flight this long: ask the stream for errors
-constexpr int64_t kEngineIdleNs = 2000000;  // no post for 2 ms: the resident engine stops
 
 // A 32-bit futex word: waiters sleep in the kernel until it changes, and one
 // wake releases all of them together.
@@ -124,7 +119,6 @@ struct Batch {
   volatile uint32_t* flag = nullptr;  // pinned host word the stream writes `launches` to
   uint32_t* flag_dev = nullptr;
   uint32_t launches = 0;
-  bool engine = false;  // the last launch went to the resident engine
   // guarded by the queue mutex
   State state = FREE;
   int key = -1;  // 0: encode, 1 + k: reconst_one(k), 1 + d: update (any rows),
@@ -164,25 +158,6 @@ struct xrs_queue {
   bool timer = false;        // XRS_QUEUE_POLICY=timer
   uint64_t spin_ns = 20000;  // launcher spin (staging fills) before yielding
   uint64_t comp_spin_ns = 200000;  // completion thread spin before yielding
-  // Resident engine (kernels.hip part 5): 12+4 codecs, vect sizes that are
-  // multiples of 32, zero-copy Encode / ReconstOne batches.  Started by the
-  // first such batch, stopped after kEngineIdleNs without one (and at
-  // teardown).  Off unless XRS_QUEUE_ENGINE=1: measured slower than launching
-  // (profiles/r03_queue_engine_ab.log).
-  bool eng_ok = false;
-  std::atomic<bool> eng_running{false};
-  void* eng_args = nullptr;
-  xrs::EngineCtl* eng_ctl = nullptr;
-  xrs::EngineCtl* eng_ctl_dev = nullptr;
-  xrs::EngineDesc* eng_ring = nullptr;
-  xrs::EngineDesc* eng_ring_dev = nullptr;
-  uint32_t* eng_count = nullptr;
-  hipStream_t eng_stream = nullptr;
-  uint32_t eng_posted = 0;
-  int eng_grid = 8;
-  uint64_t eng_idle_ticks = 100000000;  // the kernel's own idle exit: 1 s of wall clock
-  std::atomic<int64_t> eng_last{0};  // steady-clock ns of the last post
-  std::mutex eng_mu;  // posting, starting and stopping the engine
 
   // One copy between a caller's buffer and its staged stripe: `len` bytes at
   // staging row `row` (row * size + off) <-> host + off.
@@ -193,8 +168,6 @@ struct xrs_queue {
   };
 
   int launch(Batch& bt);
-  int post(Batch& bt, uint32_t op);
-  void stop_engine();
   void work();
   void complete();
   void finish(int i, int err);
@@ -235,9 +208,6 @@ int xrs_queue::launch(Batch& bt) {
   const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
                                           : rec ? static_cast<size_t>(d + p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
-  bt.engine = false;
-  if (eng_ok && zc && (enc || (!upd && !rec && !rep)))
-    if (post(bt, static_cast<uint32_t>(bt.key)) == 0) return 0;  // (else: launched below)
   uint8_t* base = zc ? bt.host_dev : bt.dev;
   int e = 0;
   if (!zc && hipMemcpy2DAsync(bt.dev + up_off, stripe_bytes, bt.host + up_off, stripe_bytes, up_len,
@@ -270,49 +240,6 @@ int xrs_queue::launch(Batch& bt) {
     e = XRS_ERR_HIP;
   if (e) (void)hipStreamSynchronize(bt.stream);  // nothing of it may still run
   return e;
-}
-
-// Post batch bt (op 0: Encode, 1 + k: ReconstOne(k)) to the resident engine,
-// starting it if needed.  Nonzero: the engine could not be started (the
-// caller launches the batch instead).
-int xrs_queue::post(Batch& bt, uint32_t op) {
-  std::lock_guard<std::mutex> g(eng_mu);
-  const int64_t now = Clock::now().time_since_epoch().count();
-  // (the kernel leaves by itself after 1 s without a descriptor; the host
-  // stops it after kEngineIdleNs, so this only matters if that did not run)
-  if (eng_running && now - eng_last.load() > 500000000 &&
-      hipStreamQuery(eng_stream) == hipSuccess)
-    eng_running = false;
-  if (!eng_running) {
-    __atomic_store_n(&eng_ctl->head, 0u, __ATOMIC_RELAXED);
-    __atomic_store_n(&eng_ctl->stop, 0u, __ATOMIC_RELAXED);
-    eng_posted = 0;
-    if (xrs::engine_launch(eng_args, eng_ctl_dev, eng_ring_dev, eng_count, eng_grid,
-                           eng_idle_ticks, eng_stream) != 0)
-      return XRS_ERR_HIP;
-    eng_running = true;
-  }
-  xrs::EngineDesc& d = eng_ring[eng_posted % xrs::kEngineRing];
-  d.slot = static_cast<uint32_t>(&bt - b);
-  d.op = op;
-  d.n = static_cast<uint32_t>(bt.n);
-  d.seq = ++bt.launches;
-  d.flag = reinterpret_cast<uint64_t>(bt.flag_dev);
-  __atomic_store_n(&eng_ctl->head, ++eng_posted, __ATOMIC_RELEASE);  // after the descriptor
-  eng_last.store(now);
-  bt.engine = true;
-  return 0;
-}
-
-// Stop the resident engine once everything posted is done (it leaves its loop
-// when it has caught up with head and sees stop).
-void xrs_queue::stop_engine() {
-  std::lock_guard<std::mutex> g(eng_mu);
-  if (!eng_running) return;
-  __atomic_store_n(&eng_ctl->stop, 1u, __ATOMIC_RELEASE);
-  (void)hipStreamSynchronize(eng_stream);
-  __atomic_store_n(&eng_ctl->stop, 0u, __ATOMIC_RELAXED);
-  eng_running = false;
 }
 
 // Batch i's results are in staging (or it failed): release its callers.
@@ -364,13 +291,6 @@ void xrs_queue::work() {
     }
     if (pick < 0) {
       if (stop && !pending) break;
-      if (eng_running.load() && in_flight == 0 &&
-          Clock::now().time_since_epoch().count() - eng_last.load() > kEngineIdleNs) {
-        lk.unlock();
-        stop_engine();
-        lk.lock();
-        continue;
-      }
       cv_work.wait_until(lk, next);
       continue;
     }
@@ -427,7 +347,7 @@ void xrs_queue::complete() {
         if (*bt.flag == bt.launches) {
           err = 0;
         } else if (poll && ns_since(bt.launched) > kStuckNs) {
-          const hipError_t q = hipStreamQuery(bt.engine ? eng_stream : bt.stream);
+          const hipError_t q = hipStreamQuery(bt.stream);
           if (q == hipSuccess) err = *bt.flag == bt.launches ? 0 : XRS_ERR_HIP;
           else if (q != hipErrorNotReady) err = XRS_ERR_HIP;
         }
@@ -521,27 +441,6 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   return err;
 }
 
-// The resident engine's stream must own its hardware queue: streams beyond
-// GPU_MAX_HW_QUEUES share queues, and a kernel queued behind the resident one
-// on a shared queue waits until it leaves (tools/persist_probe.hip `block`:
-// 4 of 8 other streams stalled for an ordinary stream, none for a CU-masked or
-// a greatest-priority one, profiles/r03_persist_probe.log).  A CU-masked
-// stream (every CU) gets a queue of its own; the greatest-priority stream is
-// the fallback.
-static hipError_t engine_stream(hipStream_t* s) {
-  hipDeviceProp_t prop;
-  int dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-      prop.multiProcessorCount > 0) {
-    std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, ~0u);
-    if (hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess)
-      return hipSuccess;
-  }
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return hipErrorInvalidValue;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-}
-
 extern "C" {
 
 int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes, int max_wait_us,
@@ -604,48 +503,6 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     }
     bt.rows_dev = static_cast<int32_t*>(dp);
   }
-  const char* ev = std::getenv("XRS_QUEUE_ENGINE");
-  if (!e && (ev && ev[0] == '1') && q->d == 12 && q->p == 4 && size % 32 == 0 &&
-      q->zc_max >= q->stripe_bytes) {
-    // one argument block per staging slot, from the plans the launched path
-    // would run on that slot (captured, not launched)
-    std::vector<xrs::PairPlan> enc_all, enc;
-    std::vector<xrs::RowsPlan> rec_all, rec;
-    std::vector<int> cnt;
-    bool ok = true;
-    for (int i = 0; i < q->n_batches && ok; ++i) {
-      ok = q->b[i].host_dev &&
-           xrs_detail::capture_plans(codec, q->b[i].host_dev, size, q->stripe_bytes, &enc, &rec,
-                                     &cnt) == XRS_OK &&
-           enc.size() == 1 && rec.size() == static_cast<size_t>(q->d);
-      for (int c : cnt) ok = ok && c == 1;
-      if (ok) {
-        enc_all.push_back(enc[0]);
-        rec_all.insert(rec_all.end(), rec.begin(), rec.end());
-      }
-    }
-    void* cp = nullptr;
-    void* rp = nullptr;
-    int khz = 0;
-    if (ok && xrs::engine_prepare(enc_all.data(), rec_all.data(), q->n_batches, q->d, &q->eng_args) == 0 &&
-        hipHostMalloc(reinterpret_cast<void**>(&q->eng_ctl), sizeof(xrs::EngineCtl), hipHostMallocMapped) == hipSuccess &&
-        hipHostGetDevicePointer(&cp, q->eng_ctl, 0) == hipSuccess &&
-        hipHostMalloc(reinterpret_cast<void**>(&q->eng_ring), sizeof(xrs::EngineDesc) * xrs::kEngineRing,
-                      hipHostMallocMapped) == hipSuccess &&
-        hipHostGetDevicePointer(&rp, q->eng_ring, 0) == hipSuccess &&
-        hipMalloc(reinterpret_cast<void**>(&q->eng_count), sizeof(uint32_t) * xrs::kEngineRing) == hipSuccess &&
-        engine_stream(&q->eng_stream) == hipSuccess) {
-      std::memset(q->eng_ctl, 0, sizeof(xrs::EngineCtl));
-      std::memset(q->eng_ring, 0, sizeof(xrs::EngineDesc) * xrs::kEngineRing);
-      q->eng_ctl_dev = static_cast<xrs::EngineCtl*>(cp);
-      q->eng_ring_dev = static_cast<xrs::EngineDesc*>(rp);
-      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
-        q->eng_idle_ticks = static_cast<uint64_t>(khz) * 1000;  // 1 s
-      q->eng_grid = env_int("XRS_QUEUE_ENGINE_GRID", 1, 64, 8);
-      q->eng_ok = true;
-    }
-    // (without the engine every batch is launched: nothing else changes)
-  }
   if (prev >= 0) (void)hipSetDevice(prev);
   if (e) {
     xrs_queue_free(q);
@@ -681,12 +538,6 @@ void xrs_queue_free(xrs_queue* q) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (q->device >= 0) (void)hipSetDevice(q->device);
-  q->stop_engine();
-  if (q->eng_stream) (void)hipStreamDestroy(q->eng_stream);
-  xrs::engine_release(q->eng_args);
-  if (q->eng_count) (void)hipFree(q->eng_count);
-  if (q->eng_ctl) (void)hipHostFree(q->eng_ctl);
-  if (q->eng_ring) (void)hipHostFree(q->eng_ring);
   for (Batch& bt : q->b) {
     if (bt.stream) (void)hipStreamDestroy(bt.stream);
     if (bt.dev) (void)hipFree(bt.dev);
@@ -852,22 +703,13 @@ size_t xrs_queue_dump(xrs_queue* q, char* buf, size_t cap) {
                 lk.owns_lock() ? "taken" : "BUSY", q->open, q->in_flight, q->inflight_bits.load(),
                 q->active.load(), q->stop ? 1 : 0);
   out += line;
-  if (q->eng_ok) {
-    std::snprintf(line, sizeof line, "engine running %d posted %u head %u stop %u seen %u polls %u\n",
-                  q->eng_running.load() ? 1 : 0, q->eng_posted,
-                  __atomic_load_n(&q->eng_ctl->head, __ATOMIC_RELAXED),
-                  __atomic_load_n(&q->eng_ctl->stop, __ATOMIC_RELAXED),
-                  __atomic_load_n(&q->eng_ctl->seen, __ATOMIC_RELAXED),
-                  __atomic_load_n(&q->eng_ctl->polls, __ATOMIC_RELAXED));
-    out += line;
-  }
   for (int i = 0; i < q->n_batches; ++i) {
     const Batch& bt = q->b[i];
     std::snprintf(line, sizeof line,
                   "batch %d %s key %d reserved %zu n %zu filled %u released %u done %u launches %u "
-                  "flag %u err %d engine %d\n",
+                  "flag %u err %d\n",
                   i, names[bt.state], bt.key, bt.reserved, bt.n, bt.filled.load(), bt.released.load(),
-                  bt.done.load(), bt.launches, bt.flag ? *bt.flag : 0u, bt.err, bt.engine ? 1 : 0);
+                  bt.done.load(), bt.launches, bt.flag ? *bt.flag : 0u, bt.err);
     out += line;
   }
   if (buf && cap) {

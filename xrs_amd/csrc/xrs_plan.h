@@ -136,37 +136,6 @@ int launch_rows(const RowsPlan& plan, void* stream);
 constexpr int kStagedDecline = -1;
 int launch_staged(const StagedPlan& plan, void* stream);
 int launch_update_rows(const UpdRowsPlan& plan, void* stream);
-// The batching queue's resident engine (kernels.hip part 5, queue.cpp).
-// Host-written control words and descriptor ring live in pinned, device-mapped
-// memory; each field the other side polls sits on its own 64-B line.
-struct EngineCtl {
-  uint32_t head;  // descriptors posted (host -> device)
-  uint32_t pad0[15];
-  uint32_t stop;  // leave once everything posted is done (host -> device)
-  uint32_t pad1[15];
-  uint32_t seen;   // descriptors workgroup 0 has finished (device -> host, diagnostics)
-  uint32_t polls;  // workgroup 0's idle polls / 1024 (device -> host, diagnostics)
-  uint32_t pad2[14];
-};
-struct EngineDesc {  // read by the engine as three 64-bit words
-  uint32_t slot;  // staging slot (argument block) of the batch
-  uint32_t op;    // 0: Encode; 1 + k: ReconstOne(k)
-  uint32_t n;     // stripes
-  uint32_t seq;   // written to *flag when the batch is done
-  uint64_t flag;  // device address of the batch's host word
-  uint64_t pad;
-};
-constexpr int kEngineRing = 64;
-constexpr int kEngineUnsupported = -2;
-// Per-slot argument blocks from captured plans (enc[i]: Encode of slot i;
-// rec[i * d + k]: ReconstOne(k) of slot i) in device memory.  The engine
-// covers 12+4 with halves that are multiples of 16 bytes; anything else
-// returns kEngineUnsupported.
-int engine_prepare(const PairPlan* enc, const RowsPlan* rec, int n_slots, int d, void** dev_args);
-// count: kEngineRing device words (zeroed here, on the stream, before the launch).
-int engine_launch(const void* dev_args, EngineCtl* ctl, const EngineDesc* ring, uint32_t* count,
-                  int grid, uint64_t idle_ticks, void* stream);
-void engine_release(void* dev_args);
 // Launch trace (diagnostics): record every kernel instantiation launched from
 // here on (on: clears the record); traced_kernels writes "name count" lines.
 void trace_kernels(bool on);

@@ -53,10 +53,13 @@ def main():
                                                          list(range(lo)), s)))
             continue
         shard, stripe = xrs_amd.batch_strides(size, D + P)
+        off = 0
         if os.environ.get("LAYOUT") == "packed":  # shards back to back at any size
             shard, stripe = size, (D + P) * size
-        buf = torch.randint(0, 256, (n * stripe,), dtype=torch.uint8, device="cuda")
-        base = buf.data_ptr()
+        if os.environ.get("LAYOUT") == "layout":  # xrs_batch_layout: strides + base offset
+            shard, stripe, off = xrs_amd.batch_layout(size, D + P)
+        buf = torch.randint(0, 256, (n * stripe + 16,), dtype=torch.uint8, device="cuda")
+        base = buf.data_ptr() + off
         cases.append((f"encode_{size}", (D + P) * size * n, buf,
                       lambda b=base, sz=size, sh=shard, st=stripe, nn=n:
                       x.encode_batched(b, sz, sh, st, nn, s)))

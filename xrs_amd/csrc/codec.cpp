@@ -7,8 +7,11 @@
 // (xrs_plan.h), and the per-stripe synchronous API that moves host vects
 // through device staging.  Every byte of shard arithmetic runs in kernels.hip.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +46,11 @@ struct xrs_codec {
   mutable uint8_t* hstaging_dev = nullptr;  // its device address (zero-copy kernels)
   mutable size_t hstaging_cap = 0;
   mutable hipStream_t stream = nullptr;
+  // completion word of the sync calls: the stream writes ++done_seq into
+  // pinned host memory after a call's work, and the caller spins on it
+  mutable uint32_t* done_word = nullptr;
+  mutable uint32_t* done_word_dev = nullptr;
+  mutable uint32_t done_seq = 0;
 
   // host-resident pipeline state (lazy; guarded by pipe_mu): kPipe device
   // slots, one stream each, so chunk i+1's H2D, chunk i's kernel and chunk
@@ -625,7 +633,47 @@ int ensure_hstaging(const xrs_codec* x, size_t bytes) {
   return XRS_OK;
 }
 
-int sync(const xrs_codec* x) { return hip_err(hipStreamSynchronize(x->stream)); }
+// Wait for everything enqueued on the sync stream.  The stream writes a fresh
+// sequence number into a pinned host word after the call's work and the
+// caller spins on it: a blocking stream sync sees a small call done several
+// us later (a spinning hipStreamQuery sees an empty kernel done 12-16 us after
+// its launch call, a host word written by the stream 7.4 us after:
+// tools/qlat_probe.hip, profiles/r03_queue_latency_probe.log).  A stream that
+// has not written the word after kSpinNs gets a hipStreamSynchronize, which
+// also reports a failed launch.  XRS_SYNC_WAIT=block: the plain sync (A/B).
+int sync(const xrs_codec* x) {
+  constexpr uint64_t kSpinNs = 2000000;
+  static const bool block = [] {
+    const char* v = std::getenv("XRS_SYNC_WAIT");
+    return v && std::strcmp(v, "block") == 0;
+  }();
+  if (!block && !x->done_word) {
+    void* dp = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&x->done_word), 64, hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer(&dp, x->done_word, 0) == hipSuccess) {
+      *x->done_word = x->done_seq;
+      x->done_word_dev = static_cast<uint32_t*>(dp);
+    } else if (x->done_word) {
+      (void)hipHostFree(x->done_word);
+      x->done_word = nullptr;
+    }
+  }
+  if (block || !x->done_word ||
+      hipStreamWriteValue32(x->stream, x->done_word_dev, ++x->done_seq, 0) != hipSuccess)
+    return hip_err(hipStreamSynchronize(x->stream));
+  volatile uint32_t* w = x->done_word;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; *w != x->done_seq; ++i) {
+    _mm_pause();
+    if ((i & 255) == 255 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) {
+      const int e = hip_err(hipStreamSynchronize(x->stream));
+      return e ? e : (*w == x->done_seq ? XRS_OK : XRS_ERR_HIP);
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);  // outputs after the word
+  return XRS_OK;
+}
 
 size_t env_size(const char* name, size_t dflt) {
   const char* v = std::getenv(name);
@@ -958,6 +1006,7 @@ void xrs_free(xrs_codec* x) {
     if (x->stream) (void)hipStreamDestroy(x->stream);
     if (x->staging) (void)hipFree(x->staging);
     if (x->hstaging) (void)hipHostFree(x->hstaging);
+    if (x->done_word) (void)hipHostFree(x->done_word);
     for (int i = 0; i < xrs_codec::kPipe; ++i) {
       if (x->pstream[i]) (void)hipStreamDestroy(x->pstream[i]);
       if (x->slot[i]) (void)hipFree(x->slot[i]);

@@ -370,3 +370,53 @@ def test_queue_mixed_ops_fuzz(d, p, size):
         t.join()
     q.close()
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("env", [
+    {"XRS_QUEUE_INFLIGHT": "1"},
+    {"XRS_QUEUE_INFLIGHT": "8", "XRS_QUEUE_BATCHES": "10"},
+    {"XRS_QUEUE_WORKERS": "3"},
+    {"XRS_QUEUE_POLICY": "timer"},
+    {"XRS_QUEUE_ZC_MAX": "0"},  # every batch through H2D / kernel / D2H
+])
+def test_queue_policies_bit_exact(env, monkeypatch):
+    """The queue's knobs (read at xrs_queue_new) change batching, never
+    results: Encode + ReconstOne from 24 threads, bit-exact to the oracle,
+    and every staging batch FREE again afterwards (xrs_queue_dump)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    size = 4096
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=16, max_wait_us=50)
+    errors = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(5000 + t))
+        try:
+            for i in range(12):
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+                ref = [a.copy() for a in v]
+                o.encode(ref)
+                q.encode(v)
+                assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, i)
+                k = int(rng.integers(0, D))
+                v[k][:] = 0x77
+                q.reconst_one(v, k)
+                assert np.array_equal(v[k], ref[k]), ("rec", t, i, k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a caller hung:\n" + q.dump()
+    assert not errors, errors[:3]
+    st = q.stats()
+    assert st["stripes"] == 24 * 12 * 2, st
+    dump = q.dump()
+    batches = [ln for ln in dump.splitlines() if ln.startswith("batch ")]
+    assert batches and all(" FREE " in ln for ln in batches), dump
+    assert "in_flight 0" in dump and "active 0" in dump, dump
+    q.close()

@@ -561,3 +561,11 @@ class XRSQueue:
         out = (ctypes.c_uint64 * 4)()
         _raise(_lib.xrs_queue_stats(self._h, out))
         return {"batches": out[0], "stripes": out[1], "run_ns": out[2], "wait_ns": out[3]}
+
+    def dump(self) -> str:
+        """The queue's state as text (xrs_queue_dump): per staging batch its
+        state, reserved / staged / released slots, launches and completion word."""
+        n = _lib.xrs_queue_dump(self._h, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        _lib.xrs_queue_dump(self._h, buf, n + 1)
+        return buf.value.decode()

@@ -420,3 +420,49 @@ def test_queue_policies_bit_exact(env, monkeypatch):
     assert batches and all(" FREE " in ln for ln in batches), dump
     assert "in_flight 0" in dump and "active 0" in dump, dump
     q.close()
+
+
+@pytest.mark.parametrize("size", [4096, 1030, 65536])
+def test_shared_codec_concurrent_sync_calls(size):
+    """The plain per-stripe calls (x.encode / x.reconst_one / x.update, the
+    cgo shim's path) from 16 threads on ONE codec: contended calls go through
+    the codec's automatic queue (codec.cpp auto_queue), the rest run
+    directly; every result is bit-exact to the oracle."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    errors = []
+    olock = threading.Lock()
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(7000 + t))
+        try:
+            for i in range(10):
+                v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+                ref = [a.copy() for a in v]
+                with olock:
+                    o.encode(ref)
+                x.encode(v)
+                assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, i)
+                row = int(rng.integers(0, D))
+                new = rng.integers(0, 256, size=size, dtype=np.uint8)
+                ref2 = [a.copy() for a in ref]
+                ref2[row] = new.copy()
+                with olock:
+                    o.encode(ref2)
+                par = v[D:]
+                x.update(v[row], new, row, par)
+                assert all(np.array_equal(a, b) for a, b in zip(par, ref2[D:])), ("upd", t, i)
+                v[row] = new
+                k = int(rng.integers(0, D))
+                v[k][:] = 0
+                x.reconst_one(v, k)
+                assert np.array_equal(v[k], ref2[k]), ("rec", t, i, k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a caller hung"
+    assert not errors, errors[:3]

@@ -91,6 +91,52 @@ int main(int argc, char** argv) {
     std::_Exit(rc);
   }
   const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
+  // `sync_bench SIZE syncmt [THREADS...]`: T threads calling the plain
+  // per-stripe xrs_encode / xrs_update on ONE codec (the drop-in call
+  // pattern; contended calls go through the codec's auto queue)
+  if (argc > 2 && std::strcmp(argv[2], "syncmt") == 0) {
+    std::vector<int> tl = {1, 8, 32};
+    if (argc > 3) {
+      tl.clear();
+      for (int i = 3; i < argc; ++i) tl.push_back(std::atoi(argv[i]));
+    }
+    for (int upd = 0; upd < 2; ++upd)
+      for (int threads : tl) {
+        std::atomic<long> total{0};
+        std::atomic<bool> stop{false};
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+          th.emplace_back([&, t] {
+            std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, (uint8_t)t));
+            std::vector<uint8_t*> p;
+            for (auto& x : v) p.push_back(x.data());
+            long n = 0;
+            while (!stop.load(std::memory_order_relaxed)) {
+              const int rc = upd ? xrs_update(c, p[t % 12], p[(t + 1) % 12], size, t % 12, p.data() + 12, 4)
+                                 : xrs_encode(c, p.data(), 16, size);
+              if (rc) {
+                std::printf("call failed: %d\n", rc);
+                std::fflush(stdout);
+                std::_Exit(5);
+              }
+              ++n;
+            }
+            total += n;
+          });
+        const double t0 = now();
+        std::this_thread::sleep_for(std::chrono::seconds(seconds));
+        stop = true;
+        for (auto& x : th) x.join();
+        const double dt = now() - t0;
+        std::printf("{\"api\": \"%s (per-stripe, shared codec)\", \"vect_bytes\": %zu, \"threads\": %d, "
+                    "\"calls_per_s\": %.0f, \"gibps\": %.3f}\n", upd ? "xrs_update" : "xrs_encode", size,
+                    threads, total / dt, total * (upd ? 10.0 : 16.0) * size / dt / (1 << 30));
+        std::fflush(stdout);
+      }
+    xrs_free(c);
+    std::fflush(stdout);
+    std::_Exit(0);
+  }
   // --- plain sync calls, one thread
   if (!(argc > 2 && std::strcmp(argv[2], "queue") == 0)) {
     std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, 1));

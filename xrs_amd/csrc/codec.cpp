@@ -51,6 +51,10 @@ struct xrs_codec {
   mutable uint32_t* done_word = nullptr;
   mutable uint32_t* done_word_dev = nullptr;
   mutable uint32_t done_seq = 0;
+  // batching queues of concurrent per-stripe calls, one per vect size
+  // (auto_queue; guarded by aq_mu)
+  mutable std::mutex aq_mu;
+  mutable std::vector<std::pair<size_t, xrs_queue*>> aq;
 
   // host-resident pipeline state (lazy; guarded by pipe_mu): kPipe device
   // slots, one stream each, so chunk i+1's H2D, chunk i's kernel and chunk
@@ -680,6 +684,37 @@ size_t env_size(const char* name, size_t dflt) {
   return (v && *v) ? static_cast<size_t>(std::strtoull(v, nullptr, 0)) : dflt;
 }
 
+// Concurrent per-stripe calls.  The sync calls of one codec serialize on
+// x->mu, so Encode / ReconstOne / Update called per stripe from many threads
+// (a Go server's goroutines through the cgo shim) would run one at a time,
+// 15-23 us each at 4 KiB.  A call of up to kAutoQueueMax bytes per vect that
+// finds the codec busy goes through a batching queue for its vect size
+// instead (queue.cpp; created on first use, batches of up to 4 MiB, at most
+// kAutoQueues sizes per codec), so concurrent callers share device batches;
+// a lone caller keeps the direct path.  Same arguments, same results, same
+// errors (inputs are validated before the choice).  XRS_AUTO_QUEUE=0 turns
+// it off.
+constexpr size_t kAutoQueueMax = 256u << 10;
+constexpr int kAutoQueues = 4;
+
+xrs_queue* auto_queue(const xrs_codec* x, size_t size) {
+  static const bool off = [] {
+    const char* v = std::getenv("XRS_AUTO_QUEUE");
+    return v && v[0] == '0';
+  }();
+  if (off || size > kAutoQueueMax || (size & 1) || size == 0) return nullptr;
+  std::lock_guard<std::mutex> g(x->aq_mu);
+  for (const auto& e : x->aq)
+    if (e.first == size) return e.second;
+  if (static_cast<int>(x->aq.size()) >= kAutoQueues) return nullptr;
+  const size_t stripe = static_cast<size_t>(std::max(x->d + x->p, x->p + 2)) * size;
+  xrs_queue* q = nullptr;
+  if (xrs_queue_new(x, size, std::max<size_t>(1, (4u << 20) / stripe), 50, &q) != XRS_OK)
+    return nullptr;
+  x->aq.push_back({size, q});
+  return q;
+}
+
 // The transfers of one synchronous call (xrs_encode ... xrs_replace), laid out
 // as `total` bytes of staging rows:
 //  * ZeroCopy (total <= XRS_SYNC_ZC_MAX, default 4 MiB): inputs are
@@ -1001,6 +1036,7 @@ int xrs_new(int data_num, int parity_num, xrs_codec** out) {
 
 void xrs_free(xrs_codec* x) {
   if (!x) return;
+  for (const auto& e : x->aq) xrs_queue_free(e.second);
   if (x->device >= 0) {
     DeviceGuard g(x->device);
     if (x->stream) (void)hipStreamDestroy(x->stream);
@@ -1555,7 +1591,11 @@ int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
   if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
   if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
   if (size == 0) return XRS_OK;
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::unique_lock<std::mutex> lk(x->mu, std::try_to_lock);
+  if (!lk.owns_lock()) {  // busy: concurrent callers share a queue's batches
+    if (xrs_queue* q = auto_queue(x, size)) return xrs_queue_encode(q, vects, n);
+    lk.lock();
+  }
   DeviceGuard g(x->device);
   Stage st(x, static_cast<size_t>(n) * size);
   if ((e = st.init())) return e;
@@ -1589,7 +1629,13 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
   for (auto& r : reads)
     if (!vects[r.first]) return XRS_ERR_INVALID_ARG;
   if (!vects[k]) return XRS_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::unique_lock<std::mutex> lk(x->mu, std::try_to_lock);
+  if (!lk.owns_lock()) {  // busy: concurrent callers share a queue's batches
+    // (the queue takes every vect; vects outside the need set may be null here)
+    xrs_queue* q = vects_ok(vects, n) ? auto_queue(x, size) : nullptr;
+    if (q) return xrs_queue_reconst_one(q, vects, n, k);
+    lk.lock();
+  }
   DeviceGuard g(x->device);
   Stage st(x, static_cast<size_t>(n) * size);
   if ((e = st.init())) return e;
@@ -1648,7 +1694,12 @@ int xrs_update(const xrs_codec* x, const uint8_t* old_data, const uint8_t* new_d
   if (!old_data || !new_data || !vects_ok(parity, n_parity)) return XRS_ERR_INVALID_ARG;
   if (size == 0) return XRS_OK;
   const int p = x->p;
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::unique_lock<std::mutex> lk(x->mu, std::try_to_lock);
+  if (!lk.owns_lock()) {  // busy: concurrent callers share a queue's batches
+    if (xrs_queue* q = auto_queue(x, size))
+      return xrs_queue_update(q, old_data, new_data, row, parity, n_parity);
+    lk.lock();
+  }
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, p old, p+1 new
   const size_t stride = static_cast<size_t>(p + 2) * size;

@@ -33,8 +33,9 @@ After the headline timed region, the same line carries:
   * "host_e2e": the host-resident path (shards start and end in pinned host
     memory, xrs_*_host, PCIe-inclusive) on every rank at once;
   * "per_stripe_queue" (N = 1): the reference's per-stripe Encode call from
-    32 caller threads through the batching queue (tools/sync_bench child,
-    host-resident 4 KiB stripes, PCIe-inclusive);
+    32 caller threads through the batching queue, and ("plain_api") the plain
+    xrs_encode / xrs_update per stripe from 32 threads on one codec
+    (tools/sync_bench children, host-resident 4 KiB stripes, PCIe-inclusive);
   * "xgmi_repair" (two or more visible GPUs): rank 0 (in a child process)
     rebuilds a data shard with half of its need set on the peer GPU (xGMI
     reads), checked bit for bit against the rebuild from local shards.
@@ -646,18 +647,30 @@ def per_stripe_queue(args):
     exe = os.path.join(ROOT, "tools", "sync_bench")
     if not os.path.exists(exe):
         return {"skipped": "tools/sync_bench not built (build() makes it)"}
-    cmd = [exe, "4096", "queue", "50"] + [str(t) for t in args.queue_callers]
-    try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
-    except subprocess.TimeoutExpired:
-        return {"error": "timed out after 120 s"}
-    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"error": f"exit {r.returncode}", "stdout_tail": r.stdout[-400:]}
-    return {"api": "xrs_queue_encode", "vect_bytes": 4096, "codec": "12+4",
-            "by_callers": {str(x["threads"]): {k: x[k] for k in (
-                "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch",
-                "wait_us_per_batch")} for x in lines}}
+    def child(mode):
+        cmd = [exe, "4096", mode] + (["50"] if mode == "queue" else []) + [
+            str(t) for t in args.queue_callers]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            return None, {"error": "timed out after 120 s"}
+        lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return None, {"error": f"exit {r.returncode}", "stdout_tail": r.stdout[-400:]}
+        return lines, None
+
+    lines, err = child("queue")
+    out = err or {"api": "xrs_queue_encode", "vect_bytes": 4096, "codec": "12+4",
+                  "by_callers": {str(x["threads"]): {k: x[k] for k in (
+                      "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch",
+                      "wait_us_per_batch")} for x in lines}}
+    # the plain drop-in call (xrs_encode per stripe) from the same number of
+    # threads on ONE codec: contended calls batch through the codec's queue
+    lines, err = child("syncmt")
+    out["plain_api"] = err or {
+        x["api"].split()[0]: {str(x["threads"]): {"gibps": x["gibps"], "calls_per_s": x["calls_per_s"]}}
+        for x in lines}
+    return out
 
 
 def xgmi_child(args) -> int:

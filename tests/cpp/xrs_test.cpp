@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
 #include <thread>
@@ -300,6 +301,49 @@ static void TestQueue_Concurrent() {
     FATAL("Update(row=d): got \"%s\"", e.msg.c_str());
 }
 
+// Not in the reference: the plain per-stripe calls from 16 threads on ONE
+// codec (a Go server's goroutines sharing an *XRS).  Contended calls batch
+// through the codec's own queue (codec.cpp auto_queue); every result must
+// equal a second codec's, driven from one thread at a time.
+static void TestXRS_SharedCodecConcurrent() {
+  auto x = must_new(kData, kParity), y = must_new(kData, kParity);
+  std::mutex ymu;
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 16; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937_64 r(500 + t);
+      for (int i = 0; i < 30; ++i) {
+        Vects v = new_shard_matrix(kData + kParity, kShard);
+        for (int j = 0; j < kData; ++j) fill_random(r, v[j]);
+        Vects ref = v;
+        {
+          std::lock_guard<std::mutex> g(ymu);
+          if (y->Encode(ref)) ++bad;
+        }
+        if (x->Encode(v) || v != ref) ++bad;
+        const int row = static_cast<int>(r() % kData);
+        Vect nd(kShard);
+        fill_random(r, nd);
+        auto pv = xrs::slices(v, kData), pr = xrs::slices(ref, kData);
+        {
+          std::lock_guard<std::mutex> g(ymu);
+          if (y->Update(ref[row], nd, row, pr)) ++bad;
+        }
+        if (x->Update(v[row], nd, row, pv)) ++bad;
+        v[row] = nd;
+        ref[row] = nd;
+        if (v != ref) ++bad;
+        const int k = static_cast<int>(r() % kData);
+        Vects w = v;
+        std::fill(w[k].begin(), w[k].end(), 0);
+        if (x->ReconstOne(w, k) || w[k] != v[k]) ++bad;
+      }
+    });
+  for (auto& t : th) t.join();
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+}
+
 // A vect shorter or longer than vects[0] is rejected before the C ABI call
 // (which reads and writes `size` bytes of every vect): ADVICE r1.
 static void TestMismatchedVects() {
@@ -343,6 +387,7 @@ int main(int argc, char** argv) {
       {"TestXRS_Update", TestXRS_Update, true},
       {"TestXRS_Replace", TestXRS_Replace, true},
       {"TestQueue_Concurrent", TestQueue_Concurrent, true},
+      {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
   };
   for (const T& t : tests) {
     if (cpu_only && t.gpu) continue;

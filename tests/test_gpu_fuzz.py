@@ -8,6 +8,7 @@ Replace).  The GPU buffer after the call must equal the oracle applied stripe
 by stripe to a host copy, byte for byte, including every byte outside the
 shards (nothing else may be written).  Seeded; bounded to a few seconds.
 XRS_FUZZ_SEEDS=N runs N seeds per test instead of 10 (long campaigns);
+XRS_FUZZ_BASE=B starts the seeds at B (fresh cases for a new campaign);
 XRS_FUZZ_BIG=1 adds 128 KiB-1 MiB vects, XRS_FUZZ_GRID=1 full grids."""
 import os
 
@@ -23,6 +24,7 @@ pytestmark = pytest.mark.gpu
 CODECS = [(12, 4), (10, 4), (6, 3), (4, 2), (5, 5), (20, 4), (1, 2), (30, 6), (3, 9), (16, 8)]
 OPS = ["encode", "reconst_one", "reconst", "update", "replace"]
 SEEDS = int(os.environ.get("XRS_FUZZ_SEEDS", "10"))
+BASE = int(os.environ.get("XRS_FUZZ_BASE", "0"))
 
 
 BIG = os.environ.get("XRS_FUZZ_BIG") == "1"  # long campaigns: also 128 KiB-1 MiB vects
@@ -54,7 +56,7 @@ def vects_of(buf, base, s, shard, stripe, size, count, first=0):
 
 @pytest.mark.parametrize("seed", range(SEEDS))
 def test_batched_fuzz_vs_oracle(seed):
-    rng = np.random.Generator(np.random.PCG64(9000 + seed))
+    rng = np.random.Generator(np.random.PCG64(9000 + BASE + seed))
     dev = torch.device("cuda:0")
     s_ = torch.cuda.current_stream().cuda_stream
     for case in range(30):
@@ -124,7 +126,7 @@ def test_sync_fuzz_vs_oracle(seed):
     """The per-stripe sync API (host vects: separate, oddly aligned numpy
     slices, sizes spanning the zero-copy / pinned / direct staging modes) on
     random codecs and operations, against the oracle."""
-    rng = np.random.Generator(np.random.PCG64(9500 + seed))
+    rng = np.random.Generator(np.random.PCG64(9500 + BASE + seed))
     for case in range(30):
         d, p = CODECS[int(rng.integers(0, len(CODECS)))]
         size = int(rng.choice([2, 34, 4096, 4112, 65538, 300000, 600002]))

@@ -338,6 +338,31 @@ static void TestXRS_SharedCodecConcurrent() {
         Vects w = v;
         std::fill(w[k].begin(), w[k].end(), 0);
         if (x->ReconstOne(w, k) || w[k] != v[k]) ++bad;
+        // two lost (one data, one parity), both needed
+        const std::vector<int> lost = {k, kData + 1 + (i % (kParity - 1))};
+        std::vector<int> has;
+        for (int j = 0; j < kData + kParity; ++j)
+          if (!is_in(j, lost)) has.push_back(j);
+        Vects g1 = v, g2 = v;
+        for (int j : lost) {
+          std::fill(g1[j].begin(), g1[j].end(), 0x5a);
+          std::fill(g2[j].begin(), g2[j].end(), 0x5a);
+        }
+        {
+          std::lock_guard<std::mutex> g(ymu);
+          if (y->Reconst(g2, has, lost)) ++bad;
+        }
+        if (x->Reconst(g1, has, lost) || g1 != g2) ++bad;
+        // Replace of two rows with fresh data
+        const std::vector<int> rr = {row, (row + 5) % kData};
+        Vects nd2 = new_shard_matrix(2, kShard);
+        for (auto& z : nd2) fill_random(r, z);
+        Vects pq(v.begin() + kData, v.end()), ps = pq;
+        {
+          std::lock_guard<std::mutex> g(ymu);
+          if (y->Replace(xrs::slices(nd2), rr, xrs::slices(ps))) ++bad;
+        }
+        if (x->Replace(xrs::slices(nd2), rr, xrs::slices(pq)) || pq != ps) ++bad;
       }
     });
   for (auto& t : th) t.join();

@@ -424,8 +424,8 @@ def test_queue_policies_bit_exact(env, monkeypatch):
 
 @pytest.mark.parametrize("size", [4096, 1030, 65536])
 def test_shared_codec_concurrent_sync_calls(size):
-    """The plain per-stripe calls (x.encode / x.reconst_one / x.update, the
-    cgo shim's path) from 16 threads on ONE codec: contended calls go through
+    """The plain per-stripe calls (x.encode / update / reconst_one /
+    reconst / replace, the cgo shim's path) from 16 threads on ONE codec: contended calls go through
     the codec's automatic queue (codec.cpp auto_queue), the rest run
     directly; every result is bit-exact to the oracle."""
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
@@ -456,6 +456,28 @@ def test_shared_codec_concurrent_sync_calls(size):
                 v[k][:] = 0
                 x.reconst_one(v, k)
                 assert np.array_equal(v[k], ref2[k]), ("rec", t, i, k)
+                # Reconst of one data and one parity vect (both needed): the
+                # reference's side effects on surviving parity included
+                lost = [k, D + 1 + i % (P - 1)]
+                has = [j for j in range(D + P) if j not in lost]
+                g1 = [a.copy() for a in v]
+                g2 = [a.copy() for a in v]
+                for j in lost:
+                    g1[j][:] = 0x5A
+                    g2[j][:] = 0x5A
+                with olock:
+                    o.reconst(g2, has, lost)
+                x.reconst(g1, has, lost)
+                assert all(np.array_equal(a, b) for a, b in zip(g1, g2)), ("reconst", t, i)
+                # Replace of two rows with fresh data
+                rows = [row, (row + 5) % D]
+                nd = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in rows]
+                pq = [a.copy() for a in v[D:]]
+                ps = [a.copy() for a in v[D:]]
+                with olock:
+                    o.replace(nd, rows, ps)
+                x.replace(nd, rows, pq)
+                assert all(np.array_equal(a, b) for a, b in zip(pq, ps)), ("replace", t, i)
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 

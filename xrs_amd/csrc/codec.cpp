@@ -685,9 +685,9 @@ size_t env_size(const char* name, size_t dflt) {
 }
 
 // Concurrent per-stripe calls.  The sync calls of one codec serialize on
-// x->mu, so Encode / ReconstOne / Update called per stripe from many threads
-// (a Go server's goroutines through the cgo shim) would run one at a time,
-// 15-23 us each at 4 KiB.  A call of up to kAutoQueueMax bytes per vect that
+// x->mu, so Encode / ReconstOne / Reconst / Update / Replace called per
+// stripe from many threads (a Go server's goroutines through the cgo shim)
+// would run one at a time, 15-30 us each at 4 KiB.  A call of up to kAutoQueueMax bytes per vect that
 // finds the codec busy goes through a batching queue for its vect size
 // instead (queue.cpp; created on first use, batches of up to 4 MiB, at most
 // kAutoQueues sizes per codec), so concurrent callers share device batches;
@@ -1355,6 +1355,54 @@ int run_in_place(const xrs_codec* x, F&& fn) {
 
 }  // namespace
 
+namespace {
+// may_queue: a busy codec hands the call to its auto queue (the queue's own
+// fallback for calls it cannot batch comes back here with false).
+int reconst_sync(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, const int* dp_has,
+                 int n_has, const int* need, int n_need, bool may_queue) {
+  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
+    return XRS_ERR_INVALID_ARG;
+  if (n_need == 1 && need[0] < x->d) return xrs_reconst_one(x, vects, n, size, need[0]);
+  int e = check_size(size);
+  if (e) return e;
+  if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
+  if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
+  std::unique_lock<std::mutex> lk(x->mu, std::try_to_lock);
+  if (!lk.owns_lock()) {  // busy: concurrent callers share a queue's batches
+    if (xrs_queue* q = may_queue && size ? auto_queue(x, size) : nullptr)
+      return xrs_queue_reconst(q, vects, n, dp_has, n_has, need, n_need);
+    lk.lock();
+  }
+  DeviceGuard g(x->device);
+  Stage st(x, static_cast<size_t>(n) * size);
+  if ((e = st.init())) return e;
+  for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(i) * size, vects[i], size);
+  if (!e) e = st.upload();
+  if (e) {
+    (void)sync(x);
+    return e;
+  }
+  Written w;
+  const int er = reconst_impl(x, st.layout(size), size, size ? 1 : 0, dp_has, n_has, need, n_need,
+                              x->stream, &w);
+  // Copy back every half the device wrote, also when a later step failed
+  // (the reference's Reconst is not atomic either).
+  const size_t half = size / 2;
+  for (auto& h : w.halves)
+    st.out(vects[h.first] + h.second * half, static_cast<size_t>(h.first) * size + h.second * half,
+           half);
+  e = st.finish();
+  return er ? er : e;
+}
+}  // namespace
+
+namespace xrs_detail {
+int reconst_direct(const xrs_codec* x, uint8_t* const* vects, int n, size_t size,
+                   const int* dp_has, int n_has, const int* need, int n_need) {
+  return reconst_sync(x, vects, n, size, dp_has, n_has, need, n_need, false);
+}
+}  // namespace xrs_detail
+
 extern "C" {
 
 int xrs_encode_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t shard_stride,
@@ -1653,34 +1701,7 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
 // xrs.go:236-301
 int xrs_reconst(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, const int* dp_has,
                 int n_has, const int* need, int n_need) {
-  if (!x || n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
-    return XRS_ERR_INVALID_ARG;
-  if (n_need == 1 && need[0] < x->d) return xrs_reconst_one(x, vects, n, size, need[0]);
-  int e = check_size(size);
-  if (e) return e;
-  if (n != x->d + x->p) return XRS_ERR_ILLEGAL_VECTS;
-  if (!vects_ok(vects, n)) return XRS_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(x->mu);
-  DeviceGuard g(x->device);
-  Stage st(x, static_cast<size_t>(n) * size);
-  if ((e = st.init())) return e;
-  for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(i) * size, vects[i], size);
-  if (!e) e = st.upload();
-  if (e) {
-    (void)sync(x);
-    return e;
-  }
-  Written w;
-  const int er = reconst_impl(x, st.layout(size), size, size ? 1 : 0, dp_has, n_has, need, n_need,
-                              x->stream, &w);
-  // Copy back every half the device wrote, also when a later step failed
-  // (the reference's Reconst is not atomic either).
-  const size_t half = size / 2;
-  for (auto& h : w.halves)
-    st.out(vects[h.first] + h.second * half, static_cast<size_t>(h.first) * size + h.second * half,
-           half);
-  e = st.finish();
-  return er ? er : e;
+  return reconst_sync(x, vects, n, size, dp_has, n_has, need, n_need, true);
 }
 
 // xrs.go:324-346
@@ -1727,7 +1748,12 @@ int xrs_replace(const xrs_codec* x, uint8_t* const* data, const int* rows, int n
   if (!vects_ok(data, n) || !vects_ok(parity, n_parity)) return XRS_ERR_INVALID_ARG;
   if (size == 0) return XRS_OK;
   const int p = x->p;
-  std::lock_guard<std::mutex> lk(x->mu);
+  std::unique_lock<std::mutex> lk(x->mu, std::try_to_lock);
+  if (!lk.owns_lock()) {  // busy: concurrent callers share a queue's batches
+    if (xrs_queue* q = auto_queue(x, size))
+      return xrs_queue_replace(q, data, rows, n, parity, n_parity);
+    lk.lock();
+  }
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, [p, p+n) data
   const size_t stride = static_cast<size_t>(p + n) * size;

@@ -67,6 +67,9 @@ int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi);
 int codec_device(const xrs_codec* x);
 int codec_d(const xrs_codec* x);
 int codec_p(const xrs_codec* x);
+// xrs_reconst without the hand-over to a busy codec's auto queue
+int reconst_direct(const xrs_codec* x, uint8_t* const* vects, int n, size_t size,
+                   const int* dp_has, int n_has, const int* need, int n_need);
 }  // namespace xrs_detail
 
 using Clock = std::chrono::steady_clock;
@@ -636,7 +639,8 @@ int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_
     clean = need[u] >= 0 && need[u] < m && !in_has[need[u]] && !in_need[need[u]];
     if (clean) in_need[need[u]] = 1;
   }
-  if (!clean) return xrs_reconst(q->codec, vects, n, q->size, dp_has, n_has, need, n_need);
+  if (!clean)
+    return xrs_detail::reconst_direct(q->codec, vects, n, q->size, dp_has, n_has, need, n_need);
   const size_t half = q->size / 2;
   std::vector<xrs_queue::Piece> in, out;
   for (int i = 0; i < m; ++i) {

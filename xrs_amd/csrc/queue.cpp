@@ -98,18 +98,15 @@ uint64_t ns_since(Clock::time_point t0) {
       std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
 }
 
-// Spin (pause) for about `spin_ns`, then yield, until pred() holds; with
-// then_yield false, give up after spin_ns instead.
+// Spin (pause) for about `spin_ns`, then yield, until pred() holds.
 template <class F>
-void spin_until(F pred, uint64_t spin_ns, bool then_yield = true) {
+void spin_until(F pred, uint64_t spin_ns) {
   const auto t0 = Clock::now();
   for (int i = 0; !pred(); ++i) {
-    if ((i & 63) == 63 && ns_since(t0) > spin_ns) {
-      if (!then_yield) return;
+    if ((i & 63) == 63 && ns_since(t0) > spin_ns)
       std::this_thread::yield();
-    } else {
+    else
       _mm_pause();
-    }
   }
 }
 
@@ -164,7 +161,6 @@ struct xrs_queue {
   bool timer = false;        // XRS_QUEUE_POLICY=timer
   uint64_t spin_ns = 20000;  // launcher spin (staging fills) before yielding
   uint64_t comp_spin_ns = 200000;  // completion thread spin before yielding
-  uint64_t caller_spin_ns = 0;     // callers poll their batch this long before sleeping
 
   // One copy between a caller's buffer and its staged stripe: `len` bytes at
   // staging row `row` (row * size + off) <-> host + off.
@@ -434,9 +430,6 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
     std::lock_guard<std::mutex> lk(mu);
     cv_work.notify_one();
   }
-  if (caller_spin_ns)  // XRS_QUEUE_CALLER_SPIN_NS (A/B): poll before sleeping
-    spin_until([&] { return bt.done.load(std::memory_order_acquire) != seq; }, caller_spin_ns,
-               /*then_yield=*/false);
   while (bt.done.load(std::memory_order_acquire) == seq) futex_wait(&bt.done, seq);
   const int err = bt.err;
   if (!err)
@@ -484,8 +477,6 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   q->timer = pv && std::strcmp(pv, "timer") == 0;
   const char* nv = std::getenv("XRS_QUEUE_SPIN_NS");
   if (nv && *nv) q->spin_ns = std::strtoull(nv, nullptr, 0);
-  const char* cv = std::getenv("XRS_QUEUE_CALLER_SPIN_NS");
-  if (cv && *cv) q->caller_spin_ns = std::strtoull(cv, nullptr, 0);
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);

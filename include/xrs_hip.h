@@ -81,12 +81,13 @@ int xrs_get_need_vects(const xrs_codec *codec, int k, int *a_need, int *a_len, i
 
 /* ---- synchronous per-stripe calls (host memory, Go-identical semantics) -- *
  * A codec may be shared across threads.  A call (Encode, ReconstOne,
- * Reconst, Update, Replace) of up to 256 KiB vects that finds its codec
- * busy with another call is batched with its concurrent peers through an
+ * Reconst, Update, Replace) of up to 1 MiB vects that finds its codec busy
+ * with another call is batched with its concurrent peers through an
  * internal xrs_queue for its vect size (same results and errors; up to four
- * sizes per codec, each holding 24 MiB of pinned host and 24 MiB of device
- * staging until xrs_free); XRS_AUTO_QUEUE=0 in the environment turns this
- * off. */
+ * sizes per codec, each holding six staging batches of max(4 MiB, one
+ * stripe) in pinned host and in device memory until xrs_free: 24 MiB each
+ * at 4 KiB vects, 96 MiB each at 1 MiB); XRS_AUTO_QUEUE=0 in the
+ * environment turns this off. */
 /* xrs.go:103 Encode(vects): n == d+p vects of `size` bytes; parity written. */
 int xrs_encode(const xrs_codec *codec, uint8_t *const *vects, int n, size_t size);
 /* xrs.go:175 ReconstOne(vects, needReconst): rebuilds data vect k from the

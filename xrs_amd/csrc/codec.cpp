@@ -687,14 +687,15 @@ size_t env_size(const char* name, size_t dflt) {
 // Concurrent per-stripe calls.  The sync calls of one codec serialize on
 // x->mu, so Encode / ReconstOne / Reconst / Update / Replace called per
 // stripe from many threads (a Go server's goroutines through the cgo shim)
-// would run one at a time, 15-30 us each at 4 KiB.  A call of up to kAutoQueueMax bytes per vect that
-// finds the codec busy goes through a batching queue for its vect size
-// instead (queue.cpp; created on first use, batches of up to 4 MiB, at most
-// kAutoQueues sizes per codec), so concurrent callers share device batches;
-// a lone caller keeps the direct path.  Same arguments, same results, same
+// would run one at a time, 15-30 us each at 4 KiB.  A call of up to
+// kAutoQueueMax bytes per vect that finds the codec busy goes through a
+// batching queue for its vect size instead (queue.cpp; created on first use,
+// batches of 4 MiB or one stripe, at most kAutoQueues sizes per codec), so
+// concurrent callers share device batches (1 MiB vects: one stripe per
+// batch, four in flight); a lone caller keeps the direct path.  Same arguments, same results, same
 // errors (inputs are validated before the choice).  XRS_AUTO_QUEUE=0 turns
 // it off.
-constexpr size_t kAutoQueueMax = 256u << 10;
+constexpr size_t kAutoQueueMax = 1u << 20;
 constexpr int kAutoQueues = 4;
 
 xrs_queue* auto_queue(const xrs_codec* x, size_t size) {

@@ -422,7 +422,7 @@ def test_queue_policies_bit_exact(env, monkeypatch):
     q.close()
 
 
-@pytest.mark.parametrize("size", [4096, 1030, 65536])
+@pytest.mark.parametrize("size", [4096, 1030, 65536, 1 << 20])
 def test_shared_codec_concurrent_sync_calls(size):
     """The plain per-stripe calls (x.encode / update / reconst_one /
     reconst / replace, the cgo shim's path) from 16 threads on ONE codec: contended calls go through
@@ -435,7 +435,7 @@ def test_shared_codec_concurrent_sync_calls(size):
     def worker(t):
         rng = np.random.Generator(np.random.PCG64(7000 + t))
         try:
-            for i in range(10):
+            for i in range(10 if size < (1 << 20) else 3):
                 v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
                 ref = [a.copy() for a in v]
                 with olock:

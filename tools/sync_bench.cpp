@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -89,6 +91,118 @@ int main(int argc, char** argv) {
     xrs_free(c);
     std::fflush(stdout);
     std::_Exit(rc);
+  }
+  // `sync_bench stress SECONDS THREADS`: liveness soak of the queue and the
+  // shared codec.  Every thread loops over random ops for SECONDS: explicit
+  // queue calls (Encode, ReconstOne, Update, Reconst of one loss pattern,
+  // Replace of one rows set) on queues of two vect sizes, and the plain API
+  // on the shared codec (auto queue) at three sizes; queues are created and
+  // freed under load every second.  Results are not checked here (the GPU
+  // tests do that); any error or a call stuck 20 s is a failure (exit 5 / 6,
+  // with the queue dump).
+  if (argc > 1 && std::strcmp(argv[1], "stress") == 0) {
+    const int secs = argc > 2 ? std::atoi(argv[2]) : 60;
+    const int threads = argc > 3 ? std::atoi(argv[3]) : 32;
+    const size_t sizes[3] = {4096, 1030, 65536};
+    // explicit queues, replaced every second; a caller holds its slot's
+    // shared lock for the call, so a queue is freed only once idle (the
+    // Python tests cover xrs_queue_free with callers inside)
+    std::atomic<xrs_queue*> qs[2];
+    std::shared_mutex qmu[2];
+    for (int i = 0; i < 2; ++i) {
+      xrs_queue* q = nullptr;
+      if (xrs_queue_new(c, sizes[i], 64, 50, &q)) return 4;
+      qs[i] = q;
+    }
+    std::atomic<bool> stop{false};
+    std::atomic<long> calls{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&, t] {
+        uint64_t r = 0x9E3779B97F4A7C15ull * (t + 1);
+        auto rnd = [&] { r ^= r << 13; r ^= r >> 7; r ^= r << 17; return r; };
+        std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(65536, (uint8_t)t));
+        std::vector<uint8_t*> p;
+        for (auto& x : v) p.push_back(x.data());
+        const int has[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 14, 15}, need[] = {0, 13};
+        const int rows[] = {3, 7};
+        while (!stop.load(std::memory_order_relaxed)) {
+          const int op = static_cast<int>(rnd() % 10);
+          int rc = 0;
+          if (op < 5) {  // explicit queue
+            const int qi = static_cast<int>(rnd() % 2);
+            std::shared_lock<std::shared_mutex> g(qmu[qi]);
+            xrs_queue* q = qs[qi].load();
+            switch (op) {
+              case 0: rc = xrs_queue_encode(q, p.data(), 16); break;
+              case 1: rc = xrs_queue_reconst_one(q, p.data(), 16, static_cast<int>(rnd() % 12)); break;
+              case 2: rc = xrs_queue_update(q, p[1], p[2], static_cast<int>(rnd() % 12), p.data() + 12, 4); break;
+              case 3: rc = xrs_queue_reconst(q, p.data(), 16, has, 14, need, 2); break;
+              default: rc = xrs_queue_replace(q, p.data(), rows, 2, p.data() + 12, 4); break;
+            }
+          } else {  // the plain API on the shared codec
+            const size_t sz = sizes[rnd() % 3];
+            switch (op) {
+              case 5: rc = xrs_encode(c, p.data(), 16, sz); break;
+              case 6: rc = xrs_reconst_one(c, p.data(), 16, sz, static_cast<int>(rnd() % 12)); break;
+              case 7: rc = xrs_update(c, p[1], p[2], sz, static_cast<int>(rnd() % 12), p.data() + 12, 4); break;
+              case 8: rc = xrs_reconst(c, p.data(), 16, sz, has, 14, need, 2); break;
+              default: rc = xrs_replace(c, p.data(), rows, 2, sz, p.data() + 12, 4); break;
+            }
+          }
+          if (rc) {
+            std::printf("STRESS FAIL: op %d rc %d\n", op, rc);
+            std::fflush(stdout);
+            std::_Exit(5);
+          }
+          ++calls;
+        }
+      });
+    // every second: replace one explicit queue (xrs_queue_free under load),
+    // and watch for progress
+    const double t0 = now();
+    long seen = 0;
+    double t_seen = now();
+    int gen = 0;
+    while (now() - t0 < secs) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(250));
+      const long n = calls.load();
+      if (n != seen) {
+        seen = n;
+        t_seen = now();
+      } else if (now() - t_seen > 20) {
+        static char dump[8192];
+        for (int i = 0; i < 2; ++i) {
+          xrs_queue_dump(qs[i].load(), dump, sizeof dump);
+          std::printf("HANG: no call finished for 20 s; queue %d:\n%s", i, dump);
+        }
+        std::fflush(stdout);
+        std::_Exit(6);
+      }
+      if (gen % 40 == 39) {  // a progress line every 10 s
+        std::printf("stress: %.0f s, %ld calls\n", now() - t0, calls.load());
+        std::fflush(stdout);
+      }
+      if (++gen % 4 == 0) {
+        const int i = (gen / 4) % 2;
+        xrs_queue* fresh = nullptr;
+        if (xrs_queue_new(c, sizes[i], 64, 50, &fresh)) return 4;
+        xrs_queue* old;
+        {
+          std::unique_lock<std::shared_mutex> g(qmu[i]);
+          old = qs[i].exchange(fresh);
+        }
+        xrs_queue_free(old);
+      }
+    }
+    stop = true;
+    for (auto& x : th) x.join();
+    for (int i = 0; i < 2; ++i) xrs_queue_free(qs[i].load());
+    xrs_free(c);
+    std::printf("{\"stress_seconds\": %d, \"threads\": %d, \"calls\": %ld, \"queues_replaced\": %d}\n",
+                secs, threads, calls.load(), gen / 4);
+    std::fflush(stdout);
+    std::_Exit(0);
   }
   const size_t size = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 4096;
   // `sync_bench SIZE syncmt [THREADS...]`: T threads calling the plain

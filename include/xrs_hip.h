@@ -246,15 +246,20 @@ int xrs_group_replace_host(xrs_group *g, const uint8_t *data_base, size_t data_s
 
 /* ---- batching queue (per-stripe calls from many threads) --------------- *
  * Coalesces concurrent per-stripe calls (Go: many goroutines calling
- * x.Encode / x.ReconstOne / x.Update) into device batches of up to
- * max_batch_stripes (capped at 64 MiB of staging) with one H2D, one kernel
- * and one D2H per batch; a batch holds calls of one kind (Encode, ReconstOne
- * of one k, Reconst of one (dpHas, need) pattern, Replace of one rows set,
- * or Update of any rows).  A batch runs when full, or max_wait_us after
- * it opened once every reserved stripe is staged (at once when small and the
- * GPU is idle).  Each call blocks until its own stripe is done and has the
- * semantics of xrs_encode / xrs_reconst_one / xrs_update for vects of the
- * queue's `size`.  Thread-safe; one queue per (codec, vect size).
+ * x.Encode / x.ReconstOne / x.Update ...) into device batches of up to
+ * max_batch_stripes (capped at 64 MiB of staging); a batch holds calls of
+ * one kind (Encode, ReconstOne of one k, Reconst of one (dpHas, need)
+ * pattern, Replace of one rows set, or Update of any rows).  The open batch
+ * runs as soon as fewer than XRS_QUEUE_INFLIGHT (default 4) batches are in
+ * flight, or when full (XRS_QUEUE_POLICY=timer: when full, when the GPU is
+ * idle, or max_wait_us after it opened).  Batches of up to XRS_QUEUE_ZC_MAX
+ * bytes (default 4 MiB) are processed in place in pinned host memory over
+ * PCIe, larger ones with one H2D, one kernel and one D2H.  Each call blocks
+ * until its own stripe is done and has the semantics of the matching
+ * synchronous call for vects of the queue's `size`.  Thread-safe; one queue
+ * per (codec, vect size).  A queue holds XRS_QUEUE_BATCHES (default 6)
+ * staging batches, each max_batch_stripes stripes (<= 64 MiB) of pinned host
+ * and of device memory, one launcher and one completion thread.
  * xrs_queue_free: later calls fail; calls in flight complete first. */
 typedef struct xrs_queue xrs_queue;
 int xrs_queue_new(const xrs_codec *codec, size_t size, size_t max_batch_stripes, int max_wait_us,

@@ -34,7 +34,13 @@ static void measure_flag(const char* name, volatile uint32_t* flag, F launch) {
   uint32_t v = *flag;
   for (int i = 0; i < 200; ++i) {
     if (launch(++v)) std::abort();
+    const double t0 = now_us();
     while (*flag != v) {
+      if (now_us() - t0 > 1e6) {
+        std::printf("%s: no completion after 1 s\n", name);
+        std::fflush(stdout);
+        std::_Exit(9);
+      }
     }
   }
   const int reps = 3000;
@@ -131,6 +137,36 @@ int main() {
       if (int e = xrs_encode_batched(c, hdev, size, size, stripe, n, s)) return e;
       return static_cast<int>(hipStreamWriteValue32(s, flag_d, v, 0));
     });
+  }
+  // A sync call's shape: gather 48 KiB of inputs (CPU memcpy into the mapped
+  // staging), launch, completion word.  "launch first": the kernel is
+  // enqueued behind hipStreamWaitValue32 on a signal word before the gather,
+  // and the host releases it after the copy, so launch and copy overlap.
+  {
+    std::vector<uint8_t> src(12 * size, 9);
+    uint32_t* sig = nullptr;
+    const bool have_sig = hipExtMallocWithFlags(reinterpret_cast<void**>(&sig), 64, hipMallocSignalMemory) == hipSuccess;
+    measure_flag("copy 48 KiB, then encode 1 + flag", flag_h, [&](uint32_t v) {
+      std::memcpy(host, src.data(), src.size());
+      if (int e = xrs_encode_batched(c, hdev, size, size, stripe, 1, s)) return e;
+      return static_cast<int>(hipStreamWriteValue32(s, flag_d, v, 0));
+    });
+    if (have_sig) {
+      volatile uint32_t* vs = sig;
+      *vs = 0;
+      uint32_t gate = 0;
+      measure_flag("wait-value, encode 1 + flag, then copy", flag_h, [&](uint32_t v) {
+        ++gate;
+        if (hipStreamWaitValue32(s, sig, gate, hipStreamWaitValueGte, 0xffffffffu) != hipSuccess) return 7;
+        if (int e = xrs_encode_batched(c, hdev, size, size, stripe, 1, s)) return e;
+        if (hipStreamWriteValue32(s, flag_d, v, 0) != hipSuccess) return 8;
+        std::memcpy(host, src.data(), src.size());
+        __atomic_store_n(const_cast<uint32_t*>(vs), gate, __ATOMIC_RELEASE);
+        return 0;
+      });
+    } else {
+      std::printf("hipMallocSignalMemory unavailable\n");
+    }
   }
   for (size_t n : {size_t(1), size_t(16)}) {
     char nm[96];

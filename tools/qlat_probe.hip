@@ -33,7 +33,11 @@ template <class F>
 static void measure_flag(const char* name, volatile uint32_t* flag, F launch) {
   uint32_t v = *flag;
   for (int i = 0; i < 200; ++i) {
-    if (launch(++v)) std::abort();
+    if (int e = launch(++v)) {
+      std::printf("%s: launch failed (%d)\n", name, e);
+      std::fflush(stdout);
+      return;
+    }
     const double t0 = now_us();
     while (*flag != v) {
       if (now_us() - t0 > 1e6) {
@@ -165,7 +169,21 @@ int main() {
         return 0;
       });
     } else {
-      std::printf("hipMallocSignalMemory unavailable\n");
+      std::printf("hipMallocSignalMemory unavailable; trying a pinned host word\n");
+      std::fflush(stdout);
+      volatile uint32_t* vs = flag_h + 16;  // same pinned page, another line
+      *vs = 0;
+      uint32_t gate = 0;
+      measure_flag("wait-value (pinned word), encode 1 + flag, then copy", flag_h, [&](uint32_t v) {
+        ++gate;
+        if (hipStreamWaitValue32(s, flag_d + 16, gate, hipStreamWaitValueGte, 0xffffffffu) != hipSuccess)
+          return 7;
+        if (int e = xrs_encode_batched(c, hdev, size, size, stripe, 1, s)) return e;
+        if (hipStreamWriteValue32(s, flag_d, v, 0) != hipSuccess) return 8;
+        std::memcpy(host, src.data(), src.size());
+        __atomic_store_n(const_cast<uint32_t*>(vs), gate, __ATOMIC_RELEASE);
+        return 0;
+      });
     }
   }
   for (size_t n : {size_t(1), size_t(16)}) {

@@ -30,6 +30,8 @@ After the headline timed region, the same line carries:
     stripes of 1 MiB vects per rank (8,192 = 128 GiB resident per GPU; at
     N = 8 the 65,536-stripe, 1 TiB batch split 8 ways), with its own
     per-rank times;
+  * "config4": BASELINE config 4, Update and Replace(4) of 8 MiB stripes,
+    device-resident, with oracle-checked samples;
   * "host_e2e": the host-resident path (shards start and end in pinned host
     memory, xrs_*_host, PCIe-inclusive) on every rank at once;
   * "per_stripe_queue" (N = 1): the reference's per-stripe Encode call from
@@ -78,6 +80,9 @@ xdist = _load_dist()
 D, P = 12, 4
 ENC_S = 4096
 REC_S = 1 << 20
+C4_S = 8 << 20  # BASELINE config 4: Update + Replace(4) @ 8 MiB
+C4_STRIPES = 16  # CPU sample per op
+C4_ROWS = (0, 1, 2, 3)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 
@@ -99,7 +104,8 @@ def _cpu_model() -> str:
 
 def _cpu_rates(o, seconds: float, threads: int):
     """Bytes/s of the oracle's batch path on `threads` for the four bench
-    kernels, each run for seconds/4 on a bounded sample."""
+    kernels and BASELINE config 4 (Update, Replace(4) @ 8 MiB), each run for
+    seconds/6 on a bounded sample."""
     import numpy as np
 
     rng = np.random.Generator(np.random.PCG64(1))
@@ -110,7 +116,7 @@ def _cpu_rates(o, seconds: float, threads: int):
         while True:
             fn(reps)
             reps += 1
-            if time.perf_counter() - t0 > seconds / 4:
+            if time.perf_counter() - t0 > seconds / 6:
                 break
         return reps * nbytes / (time.perf_counter() - t0)
 
@@ -122,13 +128,43 @@ def _cpu_rates(o, seconds: float, threads: int):
         rates["reconst_one_" + key] = run(
             lambda i: o.reconst_one_batch(buf, size, n, i % D, threads), n * 9 * size)
         del buf
+    # config 4: 16 stripes of [old, new, 4 parity] (768 MiB) and of [4 data,
+    # 4 parity] (1 GiB) @ 8 MiB; bytes (2p+2)*S and (n+2p)*S per stripe
+    buf = rng.integers(0, 256, size=(C4_STRIPES, 2 + P, C4_S), dtype=np.uint8)
+    rates["update_8m"] = run(lambda i: o.update_batch(buf, C4_S, C4_STRIPES, i % D, threads),
+                             C4_STRIPES * (2 * P + 2) * C4_S)
+    del buf
+    buf = rng.integers(0, 256, size=(C4_STRIPES, len(C4_ROWS) + P, C4_S), dtype=np.uint8)
+    rates["replace4_8m"] = run(lambda i: o.replace_batch(buf, C4_S, C4_STRIPES, C4_ROWS, threads),
+                               C4_STRIPES * (len(C4_ROWS) + 2 * P) * C4_S)
+    del buf
     return rates
 
 
+def _cpu_counts() -> dict:
+    """nproc, the affinity set and the cgroup CPU quota (cpu.max) of this
+    process: the host's cores and the share of them this job may use."""
+    out = {"nproc": os.cpu_count() or 1}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        out["affinity"] = out["nproc"]
+    out["cgroup_quota_cpus"] = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            out["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def cpu_baseline(seconds: float, step_bytes: dict):
-    """The oracle's CPU path (AVX2 low/high-nibble tables + separate piggyback
-    pass, i.e. the reference's algorithm) on a bounded sample: 1 thread (the
-    reported value), then the box's CPU share (up to 16 threads)."""
+    """The oracle's CPU path (AVX2/AVX-512 low/high-nibble tables + separate
+    piggyback pass, i.e. the reference's algorithm) on a bounded sample: 1
+    thread (the reported value), then every CPU in this process's affinity set
+    (uncapped), and the cgroup quota's CPU count when that is smaller."""
     from oracle.oracle_c import OracleXRS, lib
 
     o = OracleXRS(D, P)
@@ -137,24 +173,30 @@ def cpu_baseline(seconds: float, step_bytes: dict):
         t_step = sum(step_bytes[k] / rates[k] for k in step_bytes)
         return sum(step_bytes.values()) / t_step / GIB
 
+    counts = _cpu_counts()
     r1 = _cpu_rates(o, seconds, 1)
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    threads = max(1, min(16, share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    rn = _cpu_rates(o, seconds / 2, threads)
+    tcounts = [counts["affinity"]]
+    q = counts["cgroup_quota_cpus"]
+    if q and int(q) >= 1 and int(q) < counts["affinity"]:
+        tcounts.append(int(q))
+    multi = []
+    for t in tcounts:
+        rn = _cpu_rates(o, seconds / 2, t)
+        multi.append({"threads": t, "value": round(mix(rn), 3),
+                      "gibps": {k: round(v / GIB, 3) for k, v in rn.items()}})
+    best = max(multi, key=lambda m: m["value"])
     return {
         "value": round(mix(r1), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
         "simd": ("scalar", "avx2", "avx512bw")[lib().oxrs_simd_level()],
-        "cpu_model": _cpu_model(),
+        "cpu_model": _cpu_model(), "cpu_counts": counts,
         "gibps": {k: round(v / GIB, 3) for k, v in r1.items()},
-        "multi_thread": {"threads": threads, "value": round(mix(rn), 3),
-                         "gibps": {k: round(v / GIB, 3) for k, v in rn.items()}},
+        "multi_thread": best, "multi_thread_all": multi,
         "sample": (f"oracle/xrs_oracle.c: Encode and ReconstOne of 16384 12+4 stripes @ 4 KiB "
-                   f"(1 GiB) and of 64 stripes @ 1 MiB (1 GiB), each repeated for "
-                   f"{seconds / 4:.1f} s on 1 thread and {seconds / 8:.1f} s on {threads} "
-                   f"threads; combined with the GPU step's byte mix"),
+                   f"(1 GiB) and of 64 stripes @ 1 MiB (1 GiB); Update and Replace(rows "
+                   f"{list(C4_ROWS)}) of {C4_STRIPES} stripes @ 8 MiB (config 4); each repeated "
+                   f"for {seconds / 6:.1f} s on 1 thread and {seconds / 12:.1f} s on each of "
+                   f"{tcounts} threads; value combines the four headline kernels with the GPU "
+                   f"step's byte mix"),
     }
 
 
@@ -166,6 +208,16 @@ def lib_sha256(path: str) -> str:
         for blk in iter(lambda: f.read(1 << 20), b""):
             h.update(blk)
     return h.hexdigest()
+
+
+def library_info(xa) -> dict:
+    """The measured binary and the tree it came from: xrs_version() carries the
+    digest of the sources the library was built from (xrs_amd/csrc/version.cpp),
+    recomputed here from this checkout."""
+    built, tree = xa.library_source_hash(), xa.source_hash()
+    return {"path": os.path.relpath(xa.LIB_PATH, ROOT), "version": xa.version(),
+            "sha256": lib_sha256(xa.LIB_PATH), "src_hash": built, "tree_src_hash": tree,
+            "built_from_tree": built == tree}
 
 
 def pmc_traffic(launch: str, kernel: str, lib_path: str):
@@ -247,6 +299,14 @@ def oracle_parity(samples):
     for key, op, k, idx, before, got in samples:
         ref = before.copy()
         for j in range(ref.shape[0]):
+            if op == "update":  # [old, new, parity]
+                o.update(ref[j, 0], ref[j, 1], k, [ref[j, 2 + r] for r in range(P)])
+                continue
+            if op == "replace4":  # [data 0..3, parity]
+                nr = len(C4_ROWS)
+                o.replace([ref[j, i] for i in range(nr)], list(C4_ROWS),
+                          [ref[j, nr + r] for r in range(P)])
+                continue
             vects = [ref[j, i] for i in range(D + P)]
             if op == "encode":
                 o.encode(vects)
@@ -273,6 +333,9 @@ def parse_args(argv=None):
     ap.add_argument("--config5-stripes", type=int, default=8192,
                     help="1 MiB stripes per rank for the config5 key (0: skip)")
     ap.add_argument("--config5-steps", type=int, default=20)  # ~3.5 s of GPU work
+    ap.add_argument("--config4-stripes", type=int, default=64,
+                    help="8 MiB stripes per op for the config4 key (0: skip)")
+    ap.add_argument("--config4-steps", type=int, default=10)
     ap.add_argument("--host-mib", type=int, default=1024,
                     help="MiB per host-resident batch for the host_e2e key (0: skip)")
     ap.add_argument("--queue-callers", type=int, nargs="*", default=[32],
@@ -498,6 +561,60 @@ def config5(R: Rank, args):
     }
 
 
+def config4(R: Rank, args):
+    """BASELINE config 4: Update (row = step mod 12) and Replace(rows 0..3) of
+    12+4 stripes of 8 MiB vects, device-resident, batched (xrs_update_batched /
+    xrs_replace_batched).  Stripe layouts: [old, new, parity 0..3] and
+    [data 0..3, parity 0..3].  Bytes per stripe are the reference's SetBytes
+    (xrs_test.go:600-680): (2p+2)*S for Update, (n+2p)*S for Replace(n).
+    Each op's first / last stripes are checked against the C oracle in the
+    checker leg (samples)."""
+    torch, x, s = R.torch, R.x, R.stream
+    S, n_upd, n_rep, nr = C4_S, args.config4_stripes, args.config4_stripes, len(C4_ROWS)
+    out, samples = {"vect_bytes": S, "replace_rows": list(C4_ROWS)}, []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn, reps):
+        fn(0)
+        R.sync()
+        e0.record()
+        for i in range(reps):
+            fn(i)
+        e1.record()
+        R.sync()
+        return e0.elapsed_time(e1) / reps / 1e3
+
+    for op, rows_per, n in (("update", 2 + P, n_upd), ("replace4", nr + P, n_rep)):
+        stripe = rows_per * S
+        buf = R.random_bytes(n * stripe, 0xC04 + len(op))
+        b = buf.data_ptr()
+        par = (2 if op == "update" else nr) * S  # parity offset in a stripe
+        if op == "update":
+            fn = lambda i: x.update_batched(b, stripe, b + S, stripe, S, i % D, b + par, S, stripe, n, s)
+            algo = n * (2 * P + 2) * S
+        else:
+            fn = lambda i: x.replace_batched(b, S, stripe, list(C4_ROWS), S, b + par, S, stripe, n, s)
+            algo = n * (nr + 2 * P) * S
+        sec = timed(fn, args.config4_steps)
+        idx = [0, n - 1]
+        view = buf.view(n, stripe)
+        R.sync()
+        before = torch.stack([view[t].view(rows_per, S) for t in idx]).cpu().numpy()
+        row = 5
+        if op == "update":
+            x.update_batched(b, stripe, b + S, stripe, S, row, b + par, S, stripe, n, s)
+        else:
+            fn(0)
+        R.sync()
+        got = torch.stack([view[t].view(rows_per, S) for t in idx]).cpu().numpy()
+        samples.append(("config4_" + op, op, row if op == "update" else -1, idx, before, got))
+        out[op] = {"stripes": n, "bytes_per_launch": algo, "ms": round(sec * 1e3, 4),
+                   "gibps": round(algo / sec / GIB, 1), "frac": round(algo / sec / 1e9 / HBM_PEAK_GBS, 4)}
+        del buf, view
+        torch.cuda.empty_cache()
+    return out, samples
+
+
 def host_e2e(R: Rank, args):
     """Shards start and end in host memory: pinned, device-mapped batches
     (xrs_host_alloc) run in place over PCIe by xrs_encode_host /
@@ -709,6 +826,11 @@ def run_rank(args, w):
     c5 = None
     if args.config5_stripes > 0:
         c5 = config5(R, args)
+    c4 = None
+    if args.config4_stripes > 0:
+        c4, c4_samples = config4(R, args)
+        if not args.no_parity:
+            samples += c4_samples
     he = host_e2e(R, args) if args.host_mib > 0 else None
     pq = None
     if w.rank == 0 and w.world == 1 and args.queue_callers:
@@ -761,6 +883,7 @@ def run_rank(args, w):
                 "encode_shard_stride": enc_shard, "reconst_shard_stride": rec_shard,
                 "parallelism": f"stripe split x{w.world}, no collective",
             },
+            "library": library_info(R.xrs_amd),
             "rank_seconds": [round(v, 6) for v in rank_seconds],
             "rank_devices": R.rank_devices,
             "shared_gpu": R.shared_gpu,
@@ -768,6 +891,7 @@ def run_rank(args, w):
             "roofline": roofline,
             "parity": parity,
             "cpu_baseline": cpu,
+            "config4": c4,
             "config5": c5,
             "host_e2e": he,
             "per_stripe_queue": pq,

@@ -86,8 +86,16 @@ int xrs_get_need_vects(const xrs_codec *codec, int k, int *a_need, int *a_len, i
  * internal xrs_queue for its vect size (same results and errors; up to four
  * sizes per codec, each holding six staging batches of max(4 MiB, one
  * stripe) in pinned host and in device memory until xrs_free: 24 MiB each
- * at 4 KiB vects, 96 MiB each at 1 MiB); XRS_AUTO_QUEUE=0 in the
- * environment turns this off. */
+ * at 4 KiB vects, 96 MiB each at 1 MiB; a vect size whose staged stripe
+ * exceeds 16 MiB is never queued, so a codec holds at most 384 MiB pinned
+ * plus 384 MiB device staging; a queue that could not be created is not
+ * retried); XRS_AUTO_QUEUE=0 in the environment turns this off.
+ * Concurrent calls on one codec may run in one device batch, each on its own
+ * staged copy of its vects: concurrent calls must not share OUTPUT buffers
+ * (two Update or Replace calls on the same parity vects at once each apply
+ * their delta to their own copy and the last copy-back wins; the Go
+ * reference leaves this a data race too).  Calls on disjoint stripes, and
+ * any number of readers of shared inputs, are safe. */
 /* xrs.go:103 Encode(vects): n == d+p vects of `size` bytes; parity written. */
 int xrs_encode(const xrs_codec *codec, uint8_t *const *vects, int n, size_t size);
 /* xrs.go:175 ReconstOne(vects, needReconst): rebuilds data vect k from the

@@ -61,6 +61,8 @@ def lib():
         L.oxrs_replace.argtypes = [P, PP, IP, I, Z, PP]
         L.oxrs_encode_batch.argtypes = [P, P, Z, Z, ctypes.c_long, I]
         L.oxrs_reconst_one_batch.argtypes = [P, P, Z, Z, ctypes.c_long, I, I]
+        L.oxrs_update_batch.argtypes = [P, P, Z, Z, ctypes.c_long, I, I]
+        L.oxrs_replace_batch.argtypes = [P, P, Z, Z, ctypes.c_long, IP, I, I]
         L.oxrs_simd_available.restype = I
         L.oxrs_simd_level.restype = I
         _lib = L
@@ -137,3 +139,15 @@ class OracleXRS:
                           threads: int = 1):
         _chk(lib().oxrs_reconst_one_batch(self._buf, buf.ctypes.data, size,
                                           (self.d + self.p) * size, n_stripes, k, threads))
+
+    def update_batch(self, buf: np.ndarray, size: int, n_stripes: int, row: int,
+                     threads: int = 1):
+        """buf: [n_stripes][2 + p][size] = old, new, parity (parity updated)."""
+        _chk(lib().oxrs_update_batch(self._buf, buf.ctypes.data, size, (2 + self.p) * size,
+                                     n_stripes, row, threads))
+
+    def replace_batch(self, buf: np.ndarray, size: int, n_stripes: int, rows, threads: int = 1):
+        """buf: [n_stripes][len(rows) + p][size] = data, parity (parity updated)."""
+        _chk(lib().oxrs_replace_batch(self._buf, buf.ctypes.data, size,
+                                      (len(rows) + self.p) * size, n_stripes, _ints(rows),
+                                      len(rows), threads))

@@ -377,12 +377,14 @@ int oxrs_simd_available(void) { return oxrs_simd_level() > 0; }
  * handled by the vector loop, remainder scalar). */
 __attribute__((target("avx2"))) static void gf_matmul_avx2(const nib_tab *tab, int nout, int nin,
                                                              const uint8_t *const *in,
-                                                             uint8_t *const *out, size_t n) {
+                                                             uint8_t *const *out, size_t n,
+                                                             int acc_out) {
   const __m256i mask = _mm256_set1_epi8(0x0f);
   size_t i = 0;
   for (; i + 32 <= n; i += 32) {
     __m256i acc[8];
-    for (int r = 0; r < nout; r++) acc[r] = _mm256_setzero_si256();
+    for (int r = 0; r < nout; r++)
+      acc[r] = acc_out ? _mm256_loadu_si256((const __m256i *)(out[r] + i)) : _mm256_setzero_si256();
     for (int j = 0; j < nin; j++) {
       __m256i v = _mm256_loadu_si256((const __m256i *)(in[j] + i));
       __m256i lo = _mm256_and_si256(v, mask);
@@ -399,7 +401,7 @@ __attribute__((target("avx2"))) static void gf_matmul_avx2(const nib_tab *tab, i
   }
   for (; i < n; i++) {
     for (int r = 0; r < nout; r++) {
-      uint8_t a = 0;
+      uint8_t a = acc_out ? out[r][i] : 0;
       for (int j = 0; j < nin; j++) {
         uint8_t s = in[j][i];
         a ^= tab[r * nin + j].lo[s & 15] ^ tab[r * nin + j].hi[s >> 4];
@@ -423,12 +425,13 @@ __attribute__((target("avx2"))) static void xor_avx2(uint8_t *dst, const uint8_t
  * three-way XOR is one vpternlogq. */
 __attribute__((target("avx512f,avx512bw"))) static void gf_matmul_avx512(
     const nib_tab *tab, int nout, int nin, const uint8_t *const *in, uint8_t *const *out,
-    size_t n) {
+    size_t n, int acc_out) {
   const __m512i mask = _mm512_set1_epi8(0x0f);
   size_t i = 0;
   for (; i + 64 <= n; i += 64) {
     __m512i acc[8];
-    for (int r = 0; r < nout; r++) acc[r] = _mm512_setzero_si512();
+    for (int r = 0; r < nout; r++)
+      acc[r] = acc_out ? _mm512_loadu_si512((const void *)(out[r] + i)) : _mm512_setzero_si512();
     for (int j = 0; j < nin; j++) {
       __m512i v = _mm512_loadu_si512((const void *)(in[j] + i));
       __m512i lo = _mm512_and_si512(v, mask);
@@ -448,7 +451,7 @@ __attribute__((target("avx512f,avx512bw"))) static void gf_matmul_avx512(
     uint8_t *out2[8];
     for (int j = 0; j < nin; j++) in2[j] = in[j] + i;
     for (int r = 0; r < nout; r++) out2[r] = out[r] + i;
-    gf_matmul_avx2(tab, nout, nin, in2, out2, n - i);
+    gf_matmul_avx2(tab, nout, nin, in2, out2, n - i, acc_out);
   }
 }
 
@@ -465,10 +468,10 @@ __attribute__((target("avx512f,avx512bw"))) static void xor_avx512(uint8_t *dst,
 #endif
 
 static void gf_matmul_scalar(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
-                             uint8_t *const *out, size_t n) {
+                             uint8_t *const *out, size_t n, int acc_out) {
   for (size_t i = 0; i < n; i++)
     for (int r = 0; r < nout; r++) {
-      uint8_t a = 0;
+      uint8_t a = acc_out ? out[r][i] : 0;
       for (int j = 0; j < nin; j++) {
         uint8_t s = in[j][i];
         a ^= tab[r * nin + j].lo[s & 15] ^ tab[r * nin + j].hi[s >> 4];
@@ -477,20 +480,26 @@ static void gf_matmul_scalar(const nib_tab *tab, int nout, int nin, const uint8_
     }
 }
 
-static void gf_matmul(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
-                      uint8_t *const *out, size_t n) {
+/* out[r] = sum_j tab[r][j] * in[j]; acc_out: out[r] ^= that sum. */
+static void gf_matmul_x(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
+                        uint8_t *const *out, size_t n, int acc_out) {
 #if defined(__x86_64__)
   const int level = oxrs_simd_level();
   if (level > 0) {
     for (int r0 = 0; r0 < nout; r0 += 8) {
       int nr = nout - r0 < 8 ? nout - r0 : 8;
-      if (level > 1) gf_matmul_avx512(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n);
-      else gf_matmul_avx2(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n);
+      if (level > 1) gf_matmul_avx512(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n, acc_out);
+      else gf_matmul_avx2(tab + (size_t)r0 * nin, nr, nin, in, out + r0, n, acc_out);
     }
     return;
   }
 #endif
-  gf_matmul_scalar(tab, nout, nin, in, out, n);
+  gf_matmul_scalar(tab, nout, nin, in, out, n, acc_out);
+}
+
+static void gf_matmul(const nib_tab *tab, int nout, int nin, const uint8_t *const *in,
+                      uint8_t *const *out, size_t n) {
+  gf_matmul_x(tab, nout, nin, in, out, n, 0);
 }
 
 static void xor_fast(uint8_t *dst, const uint8_t *src, size_t n) {
@@ -630,6 +639,105 @@ int oxrs_reconst_one_batch(const oxrs *x, uint8_t *base, size_t size, size_t str
   free(e); free(einv);
   job_t proto = {x, base, size, stripe_stride, 0, 0, k, (const nib_tab *)pl, 2};
   run_jobs(reconst_one_worker, &proto, n_stripes, threads);
+  free(pl);
+  return OXRS_OK;
+}
+
+/* Update baseline over a batch (BASELINE config 4; reference benchmark
+ * xrs_test.go:600-625).  Stripe s holds [old, new, parity 0..p-1] vects of
+ * `size` bytes at base + s * stripe_stride.  The reference's two passes:
+ * rs.Update (xrs.go:331: delta = old ^ new, parity_r ^= G[r][row] * delta, in
+ * cache blocks), then the piggyback pass over the a-half (xrs.go:340-344:
+ * bv ^= old[:half] ^ new[:half]). */
+static void *update_worker(void *arg) {
+  job_t *jb = (job_t *)arg;
+  const oxrs *x = jb->x;
+  int d = x->d, p = x->p, row = jb->k;
+  size_t size = jb->size, half = size / 2;
+  uint8_t *delta = (uint8_t *)malloc(OXRS_BLOCK);
+  int a_need[OXRS_MAX_VECTS], a_len, b_need[2];
+  oxrs_get_need_vects(x, row, a_need, &a_len, b_need);
+  for (long s = jb->s0; s < jb->s1; s++) {
+    uint8_t *st = jb->base + (size_t)s * jb->stride;
+    const uint8_t *old = st, *nw = st + size;
+    uint8_t *par[OXRS_MAX_VECTS];
+    for (int r = 0; r < p; r++) par[r] = st + (size_t)(2 + r) * size;
+    for (size_t off = 0; off < size; off += OXRS_BLOCK) {
+      size_t n = size - off < OXRS_BLOCK ? size - off : OXRS_BLOCK;
+      memcpy(delta, old + off, n);
+      xor_fast(delta, nw + off, n);
+      const uint8_t *in[1] = {delta};
+      uint8_t *out[OXRS_MAX_VECTS];
+      for (int r = 0; r < p; r++) out[r] = par[r] + off;
+      gf_matmul_x(jb->tab, p, 1, in, out, n, 1);
+    }
+    uint8_t *bv = par[b_need[1] - d] + half;
+    xor_fast(bv, old, half);
+    xor_fast(bv, nw, half);
+  }
+  free(delta);
+  return NULL;
+}
+
+int oxrs_update_batch(const oxrs *x, uint8_t *base, size_t size, size_t stripe_stride,
+                      long n_stripes, int row, int threads) {
+  if (size & 1) return OXRS_ERR_SIZE_NOT_EVEN;
+  if (row < 0 || row >= x->d) return OXRS_ERR_ILLEGAL_DATA_INDEX;
+  nib_tab tab[OXRS_MAX_VECTS];
+  for (int r = 0; r < x->p; r++) make_nib(x->gen[x->d + r][row], &tab[r]);
+  job_t proto = {x, base, size, stripe_stride, 0, 0, row, tab, x->p};
+  run_jobs(update_worker, &proto, n_stripes, threads);
+  return OXRS_OK;
+}
+
+/* Replace baseline over a batch (BASELINE config 4, Replace(n); reference
+ * benchmark xrs_test.go:627-680).  Stripe s holds [data 0..n-1, parity
+ * 0..p-1]; rows[i] is data i's row.  rs.Replace (xrs.go:370: parity_r ^=
+ * sum_i G[r][rows_i] * data_i, in cache blocks), then one piggyback pass per
+ * row (xrs.go:375-385). */
+typedef struct {
+  nib_tab tab[8 * OXRS_MAX_VECTS];
+  int n, bi[OXRS_MAX_VECTS];
+} rep_plan;
+
+static void *replace_worker(void *arg) {
+  job_t *jb = (job_t *)arg;
+  const oxrs *x = jb->x;
+  const rep_plan *pl = (const rep_plan *)jb->tab;
+  int d = x->d, p = x->p, nr = pl->n;
+  size_t size = jb->size, half = size / 2;
+  for (long s = jb->s0; s < jb->s1; s++) {
+    uint8_t *st = jb->base + (size_t)s * jb->stride;
+    uint8_t *par[OXRS_MAX_VECTS];
+    for (int r = 0; r < p; r++) par[r] = st + (size_t)(nr + r) * size;
+    for (size_t off = 0; off < size; off += OXRS_BLOCK) {
+      size_t n = size - off < OXRS_BLOCK ? size - off : OXRS_BLOCK;
+      const uint8_t *in[OXRS_MAX_VECTS];
+      uint8_t *out[OXRS_MAX_VECTS];
+      for (int i = 0; i < nr; i++) in[i] = st + (size_t)i * size + off;
+      for (int r = 0; r < p; r++) out[r] = par[r] + off;
+      gf_matmul_x(pl->tab, p, nr, in, out, n, 1);
+    }
+    for (int i = 0; i < nr; i++) xor_fast(par[pl->bi[i] - d] + half, st + (size_t)i * size, half);
+  }
+  return NULL;
+}
+
+int oxrs_replace_batch(const oxrs *x, uint8_t *base, size_t size, size_t stripe_stride,
+                       long n_stripes, const int *rows, int n, int threads) {
+  if (n < 1 || n > x->d || n > 8) return OXRS_ERR_ILLEGAL_VECTS;
+  if (size & 1) return OXRS_ERR_SIZE_NOT_EVEN;
+  rep_plan *pl = (rep_plan *)calloc(1, sizeof(rep_plan));
+  pl->n = n;
+  for (int i = 0; i < n; i++) {
+    if (rows[i] < 0 || rows[i] >= x->d) { free(pl); return OXRS_ERR_ILLEGAL_DATA_INDEX; }
+    int a_need[OXRS_MAX_VECTS], a_len, b_need[2];
+    oxrs_get_need_vects(x, rows[i], a_need, &a_len, b_need);
+    pl->bi[i] = b_need[1];
+    for (int r = 0; r < x->p; r++) make_nib(x->gen[x->d + r][rows[i]], &pl->tab[r * n + i]);
+  }
+  job_t proto = {x, base, size, stripe_stride, 0, 0, 0, (const nib_tab *)pl, x->p};
+  run_jobs(replace_worker, &proto, n_stripes, threads);
   free(pl);
   return OXRS_OK;
 }

@@ -76,6 +76,12 @@ int oxrs_encode_batch(const oxrs *x, uint8_t *base, size_t size,
                       size_t stripe_stride, long n_stripes, int threads);
 int oxrs_reconst_one_batch(const oxrs *x, uint8_t *base, size_t size,
                            size_t stripe_stride, long n_stripes, int k, int threads);
+/* Update(row): stripe s = [old, new, parity 0..p-1]; Replace(rows[0..n)):
+ * stripe s = [data 0..n-1, parity 0..p-1] (n <= 8). */
+int oxrs_update_batch(const oxrs *x, uint8_t *base, size_t size, size_t stripe_stride,
+                      long n_stripes, int row, int threads);
+int oxrs_replace_batch(const oxrs *x, uint8_t *base, size_t size, size_t stripe_stride,
+                       long n_stripes, const int *rows, int n, int threads);
 
 #ifdef __cplusplus
 }

@@ -369,6 +369,42 @@ static void TestXRS_SharedCodecConcurrent() {
   if (bad) FATAL("%d mismatches or errors", bad.load());
 }
 
+// Not in the reference: slot recycling under oversubscription.
+// Two staging batches of two stripes, one in flight, 32 callers: a batch is
+// freed and reopened while other callers of its previous use still copy out,
+// so a caller that read the batch's slot count after its own release could
+// free a batch that is running.  Every Encode is checked against a serial
+// codec.
+static void TestQueue_Oversubscribed() {
+  setenv("XRS_QUEUE_BATCHES", "2", 1);
+  setenv("XRS_QUEUE_INFLIGHT", "1", 1);
+  auto x = must_new(kData, kParity), y = must_new(kData, kParity);
+  std::unique_ptr<xrs::Queue> q;
+  Error e = xrs::Queue::New(*x, kShard, &q, 2, 0);
+  unsetenv("XRS_QUEUE_BATCHES");
+  unsetenv("XRS_QUEUE_INFLIGHT");
+  if (e) FATAL("Queue::New: %s", e.msg.c_str());
+  std::mutex ymu;
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 32; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937_64 r(900 + t);
+      for (int i = 0; i < 150; ++i) {
+        Vects v = new_shard_matrix(kData + kParity, kShard);
+        for (int j = 0; j < kData; ++j) fill_random(r, v[j]);
+        Vects ref = v;
+        {
+          std::lock_guard<std::mutex> g(ymu);
+          if (y->Encode(ref)) ++bad;
+        }
+        if (q->Encode(v) || v != ref) ++bad;
+      }
+    });
+  for (auto& t : th) t.join();
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+}
+
 // A vect shorter or longer than vects[0] is rejected before the C ABI call
 // (which reads and writes `size` bytes of every vect): ADVICE r1.
 static void TestMismatchedVects() {
@@ -412,6 +448,7 @@ int main(int argc, char** argv) {
       {"TestXRS_Update", TestXRS_Update, true},
       {"TestXRS_Replace", TestXRS_Replace, true},
       {"TestQueue_Concurrent", TestQueue_Concurrent, true},
+      {"TestQueue_Oversubscribed", TestQueue_Oversubscribed, true},
       {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
   };
   for (const T& t : tests) {

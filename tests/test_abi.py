@@ -43,6 +43,15 @@ def test_version_mentions_gfx950():
     assert b"gfx950" in xrs_amd.lib().xrs_version()
 
 
+def test_library_built_from_this_tree():
+    """xrs_version() carries the digest of the sources the .so was built from
+    (xrs_amd/csrc/version.cpp); it must equal the tree's digest, i.e. the
+    shipped library is not stale (rebuild: make -C xrs_amd/csrc)."""
+    built, tree = xrs_amd.library_source_hash(), xrs_amd.source_hash()
+    assert re.fullmatch(r"[0-9a-f]{16}", tree)
+    assert built == tree, f"libxrs_hip.so was built from sources {built}, the tree is {tree}"
+
+
 def test_new_errors():
     with pytest.raises(xrs_amd.XRSError, match="^illegal parity$"):
         xrs_amd.XRS(12, 1)

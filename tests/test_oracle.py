@@ -254,6 +254,37 @@ def test_cpu_baseline_batch_paths(monkeypatch, level, d, p):
         assert np.array_equal(host, ref), (level, size, k)
 
 
+@pytest.mark.parametrize("level", ["scalar", "avx2", "native"])
+@pytest.mark.parametrize("d,p", [(12, 4), (5, 5), (20, 3)])
+def test_cpu_baseline_update_replace_batch(monkeypatch, level, d, p):
+    """The config-4 CPU baseline (oxrs_update_batch / oxrs_replace_batch, the
+    reference's two passes per op, xrs.go:324-387) equals the per-stripe
+    restatement (oxrs_update / oxrs_replace) at every SIMD level."""
+    from oracle.oracle_c import lib
+    if level == "avx2" and lib().oxrs_simd_level() < 1:
+        pytest.skip("no AVX2")
+    if level != "native":
+        monkeypatch.setenv("OXRS_SIMD", level)
+    rng = np.random.default_rng(12)
+    o = OracleXRS(d, p)
+    for size, n, threads in ((2, 3, 1), (34, 5, 2), (4096, 7, 3), (40000, 3, 2), (65602, 2, 1)):
+        row = int(rng.integers(0, d))
+        host = rng.integers(0, 256, size=(n, 2 + p, size), dtype=np.uint8)
+        ref = host.copy()
+        for s in range(n):
+            o.update(ref[s, 0], ref[s, 1], row, [ref[s, 2 + r] for r in range(p)])
+        o.update_batch(host, size, n, row, threads)
+        assert np.array_equal(host, ref), ("update", level, size)
+        rows = [int(r) for r in rng.choice(d, size=min(4, d), replace=False)]
+        host = rng.integers(0, 256, size=(n, len(rows) + p, size), dtype=np.uint8)
+        ref = host.copy()
+        for s in range(n):
+            o.replace([ref[s, i] for i in range(len(rows))], rows,
+                      [ref[s, len(rows) + r] for r in range(p)])
+        o.replace_batch(host, size, n, rows, threads)
+        assert np.array_equal(host, ref), ("replace", level, size)
+
+
 @pytest.mark.parametrize("cls", ORACLES)
 @pytest.mark.parametrize("S", [34, 2048])
 @pytest.mark.parametrize("d,p", [(10, 4), (6, 3), (5, 5), (4, 2), (20, 4), (1, 2), (30, 6)])

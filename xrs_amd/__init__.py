@@ -18,7 +18,7 @@ import os
 import threading
 
 __all__ = ["XRS", "XRSGroup", "XRSQueue", "XRSError", "lib", "LIB_PATH", "batch_strides", "batch_layout",
-           "hip_runtimes",
+           "hip_runtimes", "source_hash", "version", "library_source_hash",
            "trace_kernels", "traced_kernels"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -201,6 +201,38 @@ def batch_layout(size: int, n_shards: int):
     a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
     _raise(_lib.xrs_batch_layout(size, n_shards, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
     return a.value, b.value, c.value
+
+
+def source_hash(root: str | None = None) -> str:
+    """The digest the Makefile embeds in xrs_version() (xrs_amd/csrc/version.cpp),
+    computed from the source tree at `root` (default: this checkout): sha256 of
+    xrs_amd/csrc's Makefile and *.cpp *.h *.hip *.map in byte order of their
+    names, then include/xrs_hip.h; first 16 hex digits."""
+    import glob
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    csrc = os.path.join(root, "xrs_amd", "csrc")
+    names = {os.path.basename(f) for pat in ("*.cpp", "*.h", "*.hip", "*.map")
+             for f in glob.glob(os.path.join(csrc, pat))} | {"Makefile"}
+    files = [os.path.join(csrc, n) for n in sorted(names, key=lambda n: n.encode())]
+    files.append(os.path.join(root, "include", "xrs_hip.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def version() -> str:
+    """xrs_version(): "xrs-hip <v> gfx950 src <source digest>"."""
+    return _lib.xrs_version().decode()
+
+
+def library_source_hash() -> str:
+    """The source digest the loaded library was built with (see source_hash)."""
+    v = version().split()
+    return v[v.index("src") + 1] if "src" in v else "unknown"
 
 
 def trace_kernels(on: bool = True) -> None:

@@ -696,6 +696,9 @@ size_t env_size(const char* name, size_t dflt) {
 // errors (inputs are validated before the choice).  XRS_AUTO_QUEUE=0 turns
 // it off.
 constexpr size_t kAutoQueueMax = 1u << 20;
+// A staged stripe of at most 16 MiB (12+4 at 1 MiB vects): each queue holds
+// at most 6 batches x max(4 MiB, one stripe) of pinned and of device staging.
+constexpr size_t kAutoQueueStripeMax = 16u << 20;
 constexpr int kAutoQueues = 4;
 
 xrs_queue* auto_queue(const xrs_codec* x, size_t size) {
@@ -704,14 +707,14 @@ xrs_queue* auto_queue(const xrs_codec* x, size_t size) {
     return v && v[0] == '0';
   }();
   if (off || size > kAutoQueueMax || (size & 1) || size == 0) return nullptr;
+  const size_t stripe = static_cast<size_t>(std::max(x->d + x->p, x->p + 2)) * size;
+  if (stripe > kAutoQueueStripeMax) return nullptr;
   std::lock_guard<std::mutex> g(x->aq_mu);
   for (const auto& e : x->aq)
-    if (e.first == size) return e.second;
+    if (e.first == size) return e.second;  // (nullptr: creation failed once, not retried)
   if (static_cast<int>(x->aq.size()) >= kAutoQueues) return nullptr;
-  const size_t stripe = static_cast<size_t>(std::max(x->d + x->p, x->p + 2)) * size;
   xrs_queue* q = nullptr;
-  if (xrs_queue_new(x, size, std::max<size_t>(1, (4u << 20) / stripe), 50, &q) != XRS_OK)
-    return nullptr;
+  if (xrs_queue_new(x, size, std::max<size_t>(1, (4u << 20) / stripe), 50, &q) != XRS_OK) q = nullptr;
   x->aq.push_back({size, q});
   return q;
 }
@@ -991,8 +994,6 @@ int xrs_format_error(int code, long long arg, char* buf, size_t buflen) {
   return n < 0 ? 0 : n;
 }
 
-const char* xrs_version(void) { return "xrs-hip 0.1 gfx950"; }
-
 int xrs_trace_kernels(int on) {
   xrs::trace_kernels(on != 0);
   return XRS_OK;
@@ -1031,6 +1032,7 @@ int xrs_new(int data_num, int parity_num, xrs_codec** out) {
   int count = 0;
   if (dev >= 0 && (hipGetDeviceCount(&count) != hipSuccess || count <= 0)) dev = -1;
   x->device = dev;
+  if (dev >= 0) (void)xrs::zero_rows(dev);  // Encode padding rows: never allocated in a launch
   *out = x;
   return XRS_OK;
 }

@@ -1585,26 +1585,13 @@ int launch_encode_ct(const PairPlan& p, hipStream_t s, std::integer_sequence<int
 // guard on the piggyback instead raised the 12+4 Encode from 170 to 258
 // VGPRs).
 constexpr int kPadRows = 3;
-constexpr uint64_t kZeroRowBytes = 1u << 20;  // >= a whole vect of every padded launch
 
-// Device address of kZeroRowBytes zero bytes on the current device (made
-// once per device, never freed: a launch in flight may read it), or 0.
-uint64_t zero_rows() {
-  static std::mutex mu;
-  static uint64_t buf[64] = {};
+// The zero rows of the device the launch stream belongs to (not the calling
+// thread's current device: a batched call may run on another GPU's stream).
+uint64_t zero_rows_for(hipStream_t s) {
   int dev = -1;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  std::lock_guard<std::mutex> g(mu);
-  if (!buf[dev]) {
-    void* p = nullptr;
-    if (hipMalloc(&p, kZeroRowBytes) != hipSuccess) return 0;
-    if (hipMemset(p, 0, kZeroRowBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(p);
-      return 0;
-    }
-    buf[dev] = reinterpret_cast<uint64_t>(p);
-  }
-  return buf[dev];
+  if (hipStreamGetDevice(s, &dev) != hipSuccess) return 0;
+  return zero_rows(dev);
 }
 
 template <int... Cs>
@@ -1640,7 +1627,7 @@ int launch_pair_c(const PairPlan& p, hipStream_t s) {
       // runtime kernel on ten codecs; from 16 KiB vects the runtime kernel is
       // as fast or faster (-10..+4%, 1 MiB -5..+2%;
       // profiles/r03_pad_ab2.log, r03_pad_ab3.log).
-      const uint64_t z = (cs > 0 && p.C > 0 && p.half <= 4096 && !pad_disabled()) ? zero_rows() : 0;
+      const uint64_t z = (cs > 0 && p.C > 0 && p.half <= 4096 && !pad_disabled()) ? zero_rows_for(s) : 0;
       if (z) {
         PairPlan q = p;
         for (int c = p.C; c < cs; ++c) {
@@ -1839,6 +1826,30 @@ bool rows_overlap(const RowRef& a, const RowRef& b, uint64_t len, uint64_t n_str
 }  // namespace
 
 #if XRS_HAS_PART(1)
+uint64_t zero_rows(int dev) {
+  constexpr uint64_t kZeroRowBytes = 1u << 20;  // >= a whole vect of every padded launch
+  static std::mutex mu;
+  static uint64_t buf[64] = {};
+  if (dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (!buf[dev]) {
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) return 0;
+    void* p = nullptr;
+    hipStream_t z = nullptr;
+    bool ok = hipMalloc(&p, kZeroRowBytes) == hipSuccess;
+    // zeroed on a private stream: no null-stream barrier against the user's work
+    ok = ok && hipStreamCreateWithFlags(&z, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMemsetAsync(p, 0, kZeroRowBytes, z) == hipSuccess && hipStreamSynchronize(z) == hipSuccess;
+    if (z) (void)hipStreamDestroy(z);
+    if (ok) buf[dev] = reinterpret_cast<uint64_t>(p);
+    else if (p) (void)hipFree(p);
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+  }
+  return buf[dev];
+}
+
 std::atomic<bool> g_trace{false};
 std::mutex g_trace_mu;
 std::vector<std::pair<std::string, uint64_t>> g_trace_log;

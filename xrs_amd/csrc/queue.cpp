@@ -431,11 +431,15 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
     cv_work.notify_one();
   }
   while (bt.done.load(std::memory_order_acquire) == seq) futex_wait(&bt.done, seq);
+  // The batch cannot be recycled before this caller's own release below, so
+  // its slot count and status are read here, once: after the release another
+  // caller may free the batch and a new submit() reopen it (n = 0).
+  const size_t n_slots = bt.n;
   const int err = bt.err;
   if (!err)
     for (const Piece& pc : out)
       std::memcpy(pc.host + pc.off, st + static_cast<size_t>(pc.row) * size + pc.off, pc.len);
-  if (bt.released.fetch_add(1, std::memory_order_acq_rel) + 1 == bt.n) {
+  if (bt.released.fetch_add(1, std::memory_order_acq_rel) + 1 == n_slots) {
     std::lock_guard<std::mutex> lk(mu);
     bt.state = FREE;
     cv_free.notify_all();

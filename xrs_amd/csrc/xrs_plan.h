@@ -140,5 +140,10 @@ int launch_update_rows(const UpdRowsPlan& plan, void* stream);
 // here on (on: clears the record); traced_kernels writes "name count" lines.
 void trace_kernels(bool on);
 size_t traced_kernels(char* buf, size_t cap);
+// Device address of the zero rows that pad an Encode to a compile-time
+// source count on device `dev` (allocated and zeroed on first call for that
+// device, never freed: a launch in flight may read it), or 0.  xrs_new calls
+// it for the codec's device so the launch path never allocates.
+uint64_t zero_rows(int dev);
 
 }  // namespace xrs

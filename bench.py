@@ -780,12 +780,16 @@ def per_stripe_queue(args):
     out = err or {"api": "xrs_queue_encode", "vect_bytes": 4096, "codec": "12+4",
                   "by_callers": {str(x["threads"]): {k: x[k] for k in (
                       "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch",
-                      "wait_us_per_batch")} for x in lines}}
+                      "wait_us_per_batch", "cpu_cores", "cpu_seconds_per_gib") if k in x}
+                      for x in lines},
+                  "cpu_note": ("cpu_cores = process CPU time (callers' copies + the queue's "
+                               "launcher and completion threads) / wall time")}
     # the plain drop-in call (xrs_encode per stripe) from the same number of
     # threads on ONE codec: contended calls batch through the codec's queue
     lines, err = child("syncmt")
     out["plain_api"] = err or {
-        x["api"].split()[0]: {str(x["threads"]): {"gibps": x["gibps"], "calls_per_s": x["calls_per_s"]}}
+        x["api"].split()[0]: {str(x["threads"]): {k: x[k] for k in (
+            "gibps", "calls_per_s", "cpu_cores", "cpu_seconds_per_gib") if k in x}}
         for x in lines}
     return out
 

@@ -14,21 +14,28 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SMALL = ["--steps", "3", "--warmup", "1", "--enc-stripes", "2048", "--rec-stripes", "16",
          "--no-cpu-baseline", "--config5-stripes", "64", "--config5-steps", "2", "--host-mib", "32",
-         "--xgmi-stripes", "4", "--ramp-seconds", "0.3"]
+         "--xgmi-stripes", "4", "--ramp-seconds", "0.3", "--config4-stripes", "4",
+         "--config4-steps", "2"]
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
-        "cpu_baseline", "parity", "rank_devices", "shared_gpu"}
-PARITY_KEYS = ("encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m")
+        "cpu_baseline", "parity", "rank_devices", "shared_gpu", "config4", "library"}
+PARITY_KEYS = ("encode_4k", "reconst_one_4k", "encode_1m", "reconst_one_1m", "config4_update",
+               "config4_replace4")
 
 
 def _check_parity(j):
     """The line's oracle parity leg: every headline launch bit-exact on its
-    sampled stripes (first / middle / last), ReconstOne at two k."""
+    sampled stripes (first / middle / last), ReconstOne at two k, and config
+    4's Update and Replace(4) on their first / last stripes; the measured
+    library is the tree's (source digest, xrs_version())."""
     par = j["parity"]
     assert par["oracle"] == "oracle/xrs_oracle.c"
     assert all(par[k] is True for k in PARITY_KEYS), par
     assert par["bitexact"] is True and all(par["all_ranks"])
-    assert len(par["cases"]) == 6 and all(c["bitexact"] for c in par["cases"])
+    assert len(par["cases"]) == 8 and all(c["bitexact"] for c in par["cases"])
+    assert j["library"]["built_from_tree"] is True, j["library"]
+    c4 = j["config4"]
+    assert c4["update"]["gibps"] > 0 and c4["replace4"]["gibps"] > 0
 
 
 def _line(out: str) -> dict:

@@ -15,6 +15,9 @@ run() {  # name seconds cmd...
   return $rc
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
+if [[ $STEPS == *counters* ]]; then
+  run counters 120 rocprofv3 -L || true
+fi
 if [[ $STEPS == *pytest* ]]; then
   run pytest_gpu 1200 python -u -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider \
       --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <mutex>
 #include <shared_mutex>
 #include <thread>
@@ -18,6 +19,14 @@
 
 static double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// CPU seconds used by the whole process (every caller thread plus the
+// library's launcher and completion threads).
+static double cpu_now() {
+  timespec ts;
+  clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
 // `sync_bench ref`: every sub-benchmark of the reference's xrs_test.go
@@ -237,14 +246,16 @@ int main(int argc, char** argv) {
             }
             total += n;
           });
-        const double t0 = now();
+        const double t0 = now(), c0 = cpu_now();
         std::this_thread::sleep_for(std::chrono::seconds(seconds));
         stop = true;
         for (auto& x : th) x.join();
-        const double dt = now() - t0;
+        const double dt = now() - t0, cpu = cpu_now() - c0;
+        const double gib = total * (upd ? 10.0 : 16.0) * size / (1 << 30);
         std::printf("{\"api\": \"%s (per-stripe, shared codec)\", \"vect_bytes\": %zu, \"threads\": %d, "
-                    "\"calls_per_s\": %.0f, \"gibps\": %.3f}\n", upd ? "xrs_update" : "xrs_encode", size,
-                    threads, total / dt, total * (upd ? 10.0 : 16.0) * size / dt / (1 << 30));
+                    "\"calls_per_s\": %.0f, \"gibps\": %.3f, \"cpu_cores\": %.2f, "
+                    "\"cpu_seconds_per_gib\": %.3f}\n", upd ? "xrs_update" : "xrs_encode", size,
+                    threads, total / dt, gib / dt, cpu / dt, gib > 0 ? cpu / gib : 0.0);
         std::fflush(stdout);
       }
     xrs_free(c);
@@ -320,7 +331,7 @@ int main(int argc, char** argv) {
         }
         total += n;
       });
-    const double t0 = now();
+    const double t0 = now(), c0 = cpu_now();
     std::this_thread::sleep_for(std::chrono::seconds(seconds));
     stop = true;
     // watchdog: callers that do not all return within 10 s are stuck
@@ -340,16 +351,18 @@ int main(int argc, char** argv) {
       std::_Exit(6);
     });
     for (auto& x : th) x.join();
-    const double dt = now() - t0;
+    const double dt = now() - t0, cpu = cpu_now() - c0;
+    const double gib = total * (upd ? 10.0 : 16.0) * size / (1 << 30);
     uint64_t st[4] = {0, 0, 0, 0};
     xrs_queue_stats(q, st);
     const double nb = st[0] ? static_cast<double>(st[0]) : 1.0;
     std::printf("{\"api\": \"%s\", \"vect_bytes\": %zu, \"threads\": %d, "
                 "\"stripes_per_s\": %.0f, \"gibps\": %.3f, \"batches\": %llu, "
                 "\"stripes_per_batch\": %.1f, \"run_us_per_batch\": %.1f, "
-                "\"wait_us_per_batch\": %.1f}\n", upd ? "xrs_queue_update" : "xrs_queue_encode",
-                size, threads, total / dt, total * (upd ? 10.0 : 16.0) * size / dt / (1 << 30), (unsigned long long)st[0], st[1] / nb,
-                st[2] / nb / 1e3, st[3] / nb / 1e3);
+                "\"wait_us_per_batch\": %.1f, \"cpu_cores\": %.2f, \"cpu_seconds_per_gib\": %.3f}\n",
+                upd ? "xrs_queue_update" : "xrs_queue_encode",
+                size, threads, total / dt, gib / dt, (unsigned long long)st[0], st[1] / nb,
+                st[2] / nb / 1e3, st[3] / nb / 1e3, cpu / dt, gib > 0 ? cpu / gib : 0.0);
     std::fflush(stdout);
     if (std::getenv("XRS_QUEUE_DUMP")) {
       static char dump[8192];

@@ -719,6 +719,10 @@ xrs_queue* auto_queue(const xrs_codec* x, size_t size) {
   return q;
 }
 
+// Base offset that puts the b-half (vect[S/2:]) of a vect staged at a 16-B
+// boundary on a 16-B boundary (xrs_batch_layout): 0 when S/2 % 16 == 0.
+size_t half_align_offset(size_t size) { return (16 - (size / 2) % 16) % 16; }
+
 // The transfers of one synchronous call (xrs_encode ... xrs_replace), laid out
 // as `total` bytes of staging rows:
 //  * ZeroCopy (total <= XRS_SYNC_ZC_MAX, default 4 MiB): inputs are
@@ -732,7 +736,11 @@ class Stage {
  public:
   enum Mode { kZeroCopy, kPinned, kDirect };
 
-  Stage(const xrs_codec* x, size_t total) : x_(x), total_(std::max<size_t>(total, 1)) {}
+  // `vect` = the call's vect size: the staged rows start at the odd-size base
+  // offset (half_align_offset), so every b-half of an odd vect size is as
+  // aligned as in a batch laid out by xrs_batch_layout.
+  Stage(const xrs_codec* x, size_t total, size_t vect)
+      : x_(x), bo_(half_align_offset(vect)), total_(std::max<size_t>(total, 1) + bo_) {}
 
   int init() {
     int e = ensure_staging(x_, mode_for() == kZeroCopy ? 1 : total_);  // also creates the stream
@@ -747,12 +755,13 @@ class Stage {
     }
     return XRS_OK;
   }
-  uint8_t* base() const { return mode_ == kZeroCopy ? x_->hstaging_dev : x_->staging; }
+  uint8_t* base() const { return (mode_ == kZeroCopy ? x_->hstaging_dev : x_->staging) + bo_; }
   Layout layout(size_t shard_stride, size_t off = 0) const { return {base() + off, shard_stride, total_}; }
 
   int in(size_t off, const void* src, size_t n) {
     if (n == 0) return XRS_OK;
     if (!src) return XRS_ERR_INVALID_ARG;
+    off += bo_;
     if (mode_ == kDirect)
       return hip_err(hipMemcpyAsync(x_->staging + off, src, n, hipMemcpyHostToDevice, x_->stream));
     std::memcpy(x_->hstaging + off, src, n);
@@ -768,6 +777,7 @@ class Stage {
   }
   void out(void* dst, size_t off, size_t n) {
     if (n == 0) return;
+    off += bo_;
     outs_.push_back({dst, off, n});
     out_lo_ = std::min(out_lo_, off);
     out_hi_ = std::max(out_hi_, off + n);
@@ -800,7 +810,8 @@ class Stage {
     return kDirect;
   }
   const xrs_codec* x_;
-  size_t total_;
+  size_t bo_;     // odd-size base offset of the staged rows (0..15)
+  size_t total_;  // staging bytes, bo_ included
   Mode mode_ = kDirect;
   size_t in_lo_ = SIZE_MAX, in_hi_ = 0, out_lo_ = SIZE_MAX, out_hi_ = 0;
   std::vector<Out> outs_;
@@ -855,7 +866,9 @@ int run_pipeline(const xrs_codec* x, const HostBatch& hb,
   const size_t chunk = std::max<size_t>(1, std::min(hb.n_stripes, kChunkBytes / dev_stripe));
   std::lock_guard<std::mutex> lk(x->pipe_mu);
   DeviceGuard g(x->device);
-  int e = ensure_pipe(x, chunk * dev_stripe);
+  // device slots start at the odd-size base offset (half_align_offset)
+  const size_t bo = half_align_offset(S);
+  int e = ensure_pipe(x, chunk * dev_stripe + bo);
   if (e) return e;
   auto piece = [&](int half, size_t* off, size_t* len) {
     *off = half == 1 ? H : 0;
@@ -865,7 +878,7 @@ int run_pipeline(const xrs_codec* x, const HostBatch& hb,
   for (size_t c0 = 0; c0 < hb.n_stripes && !e; c0 += chunk, ++i) {
     const int si = static_cast<int>(i % xrs_codec::kPipe);
     hipStream_t st = x->pstream[si];
-    uint8_t* slot = x->slot[si];
+    uint8_t* slot = x->slot[si] + bo;
     const size_t nc = std::min(chunk, hb.n_stripes - c0);
     for (auto& p : in) {
       size_t off, len;
@@ -903,19 +916,20 @@ struct HostRows {
 // (Update: old, new and parity; Replace: data and parity): chunked H2D of
 // `in`, launch(slot, n, stream) on stripes of dev_stripe bytes, D2H of `out`.
 template <class Launch>
-int run_pipeline_rows(const xrs_codec* x, size_t n_stripes, size_t dev_stripe,
+int run_pipeline_rows(const xrs_codec* x, size_t size, size_t n_stripes, size_t dev_stripe,
                       const std::vector<HostRows>& in, const std::vector<HostRows>& out,
                       Launch launch) {
   const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
   std::lock_guard<std::mutex> lk(x->pipe_mu);
   DeviceGuard g(x->device);
-  int e = ensure_pipe(x, chunk * dev_stripe);
+  const size_t bo = half_align_offset(size);  // as run_pipeline
+  int e = ensure_pipe(x, chunk * dev_stripe + bo);
   if (e) return e;
   size_t i = 0;
   for (size_t c0 = 0; c0 < n_stripes && !e; c0 += chunk, ++i) {
     const int si = static_cast<int>(i % xrs_codec::kPipe);
     hipStream_t st = x->pstream[si];
-    uint8_t* slot = x->slot[si];
+    uint8_t* slot = x->slot[si] + bo;
     const size_t nc = std::min(chunk, n_stripes - c0);
     for (const HostRows& r : in)
       if (!e)
@@ -1135,7 +1149,7 @@ int xrs_batch_layout(size_t size, int n_shards, size_t* shard_stride, size_t* st
   // profiles/r03_layout_odd.log, fraction of 8 TB/s): ReconstOne 4,100 B
   // 0.602 -> 0.684, 4,098 B 0.594 -> 0.663, 1 MiB + 2 0.643 -> 0.716;
   // 2-lost Reconst +2..+8%; Encode unchanged (reads a- and b-halves alike).
-  *base_offset = (16 - (size / 2) % 16) % 16;
+  *base_offset = half_align_offset(size);
   return XRS_OK;
 }
 
@@ -1377,7 +1391,7 @@ int reconst_sync(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, 
     lk.lock();
   }
   DeviceGuard g(x->device);
-  Stage st(x, static_cast<size_t>(n) * size);
+  Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(i) * size, vects[i], size);
   if (!e) e = st.upload();
@@ -1553,7 +1567,7 @@ int xrs_update_host(const xrs_codec* x, const uint8_t* old_base, size_t old_stri
   }
   in.push_back({const_cast<uint8_t*>(old_base), old_stripe_stride, static_cast<size_t>(p) * size, size});
   in.push_back({const_cast<uint8_t*>(new_base), new_stripe_stride, static_cast<size_t>(p + 1) * size, size});
-  return run_pipeline_rows(x, n_stripes, dev_stripe, in, out,
+  return run_pipeline_rows(x, size, n_stripes, dev_stripe, in, out,
                            [&](uint8_t* slot, size_t n, hipStream_t s) {
     return update_impl(x, {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p) * size), dev_stripe},
                        {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p + 1) * size), dev_stripe},
@@ -1596,7 +1610,7 @@ int xrs_replace_host(const xrs_codec* x, const uint8_t* data_base, size_t data_s
   for (int i = 0; i < n; ++i)
     in.push_back({const_cast<uint8_t*>(data_base) + i * data_shard_stride, data_stripe_stride,
                   static_cast<size_t>(p + i) * size, size});
-  return run_pipeline_rows(x, n_stripes, dev_stripe, in, out,
+  return run_pipeline_rows(x, size, n_stripes, dev_stripe, in, out,
                            [&](uint8_t* slot, size_t ns, hipStream_t s) {
     return replace_impl(x, {slot + static_cast<size_t>(p) * size, size, dev_stripe}, rows, n, size,
                         {slot, size, dev_stripe}, ns, s);
@@ -1648,7 +1662,7 @@ int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
     lk.lock();
   }
   DeviceGuard g(x->device);
-  Stage st(x, static_cast<size_t>(n) * size);
+  Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (int j = 0; j < x->d && !e; ++j) e = st.in(static_cast<size_t>(j) * size, vects[j], size);
   if (!e) e = st.upload();
@@ -1688,7 +1702,7 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
     lk.lock();
   }
   DeviceGuard g(x->device);
-  Stage st(x, static_cast<size_t>(n) * size);
+  Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (size_t i = 0; i < reads.size() && !e; ++i) {
     const size_t off = static_cast<size_t>(reads[i].first) * size + reads[i].second * half;
@@ -1727,7 +1741,7 @@ int xrs_update(const xrs_codec* x, const uint8_t* old_data, const uint8_t* new_d
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, p old, p+1 new
   const size_t stride = static_cast<size_t>(p + 2) * size;
-  Stage st(x, stride);
+  Stage st(x, stride, size);
   if ((e = st.init())) return e;
   for (int r = 0; r < p && !e; ++r) e = st.in(static_cast<size_t>(r) * size, parity[r], size);
   if (!e) e = st.in(static_cast<size_t>(p) * size, old_data, size);
@@ -1760,7 +1774,7 @@ int xrs_replace(const xrs_codec* x, uint8_t* const* data, const int* rows, int n
   DeviceGuard g(x->device);
   // staging rows: [0, p) parity, [p, p+n) data
   const size_t stride = static_cast<size_t>(p + n) * size;
-  Stage st(x, stride);
+  Stage st(x, stride, size);
   if ((e = st.init())) return e;
   for (int r = 0; r < p && !e; ++r) e = st.in(static_cast<size_t>(r) * size, parity[r], size);
   for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(p + i) * size, data[i], size);

@@ -142,6 +142,7 @@ struct xrs_queue {
   const xrs_codec* codec = nullptr;
   int d = 0, p = 0, device = -1;
   size_t size = 0, stripe_bytes = 0, max_batch = 1, zc_max = 0;
+  size_t bo = 0;  // staged stripes start at the odd-size base offset (b-halves aligned)
   std::chrono::microseconds max_wait{50};
   Batch b[kBatches];
   uint32_t* flags = nullptr;  // pinned, mapped: kFlagStride words per batch
@@ -211,9 +212,10 @@ int xrs_queue::launch(Batch& bt) {
   const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
                                           : rec ? static_cast<size_t>(d + p) * size : size;
   const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
-  uint8_t* base = zc ? bt.host_dev : bt.dev;
+  uint8_t* base = (zc ? bt.host_dev : bt.dev) + bo;
+  uint8_t *hst = bt.host + bo, *dst = bt.dev + bo;
   int e = 0;
-  if (!zc && hipMemcpy2DAsync(bt.dev + up_off, stripe_bytes, bt.host + up_off, stripe_bytes, up_len,
+  if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
                               n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
   if (!e) {
@@ -236,7 +238,7 @@ int xrs_queue::launch(Batch& bt) {
                                       bt.stream);
   }
   if (!e && !zc &&
-      hipMemcpy2DAsync(bt.host + dn_off, stripe_bytes, bt.dev + dn_off, stripe_bytes, dn_len, n,
+      hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
                        hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
   if (!e && hipStreamWriteValue32(bt.stream, bt.flag_dev, ++bt.launches, 0) != hipSuccess)
@@ -363,7 +365,9 @@ void xrs_queue::complete() {
       if (any) {
         idle = Clock::now();
       } else if (ns_since(idle) > comp_spin_ns) {
-        std::this_thread::yield();
+        // a long batch (large stripes over PCIe): poll every 20 us instead of
+        // burning a core (adds at most 20 us to a batch that ran > 200 us)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
       } else {
         _mm_pause();
       }
@@ -420,7 +424,7 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
     if (bp->reserved == max_batch) close_open();
   }
   Batch& bt = *bp;
-  uint8_t* st = bt.host + slot * stripe_bytes;
+  uint8_t* st = bt.host + bo + slot * stripe_bytes;
   if (row >= 0) bt.rows[slot] = row;
   for (const Piece& pc : in)
     std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
@@ -465,6 +469,9 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   // A staged stripe holds d+p vects (Encode, ReconstOne) or p parity + old +
   // new (Update): p+2 rows, more than d+p only when d == 1.
   q->stripe_bytes = static_cast<size_t>(std::max(q->d + q->p, q->p + 2)) * size;
+  // xrs_batch_layout's base offset: with an odd half (size % 32 != 0) every
+  // staged b-half is as aligned as in a recommended device batch
+  q->bo = (16 - (size / 2) % 16) % 16;
   q->max_batch = std::max<size_t>(
       1, std::min(max_batch_stripes ? max_batch_stripes : SIZE_MAX, kMaxBatchBytes / q->stripe_bytes));
   q->max_wait = std::chrono::microseconds(max_wait_us);
@@ -495,8 +502,8 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     bt.flag = q->flags + i * kFlagStride;
     *bt.flag = 0;
     bt.flag_dev = static_cast<uint32_t*>(fp) + i * kFlagStride;
-    if (hipHostMalloc(&bt.host, q->max_batch * q->stripe_bytes, hipHostMallocMapped) != hipSuccess ||
-        hipMalloc(&bt.dev, q->max_batch * q->stripe_bytes) != hipSuccess ||
+    if (hipHostMalloc(&bt.host, q->max_batch * q->stripe_bytes + q->bo, hipHostMallocMapped) != hipSuccess ||
+        hipMalloc(&bt.dev, q->max_batch * q->stripe_bytes + q->bo) != hipSuccess ||
         hipStreamCreateWithFlags(&bt.stream, hipStreamNonBlocking) != hipSuccess) {
       e = XRS_ERR_HIP;
       break;

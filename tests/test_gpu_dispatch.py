@@ -53,13 +53,13 @@ def test_headline_shapes(codec, size, n, enc, rec):
 
 # (lost = needed, every survivor in dpHas) -> the staged kernel that runs
 STAGED = [
-    ([2, 9], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1, true>"),
-    ([0, 1, 2], 4096, "staged_ws_kernel<12, 13, 3, 3, 256, 1, true>"),
-    ([12], 4096, "staged_ws_kernel<12, 15, 1, 1, 256, 1, true>"),
-    ([13], 4096, "staged_ws_kernel<12, 14, 1, 1, 256, 1, true>"),
-    ([15], 1 << 20, "staged_ws_kernel<12, 14, 1, 1, 512, 1, true>"),
-    ([12], 1 << 20, "staged_ws_kernel<12, 15, 1, 1, 512, 1, true>"),
-    ([0, 13], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1, true>"),
+    ([2, 9], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1>"),
+    ([0, 1, 2], 4096, "staged_ws_kernel<12, 13, 3, 3, 256, 1>"),
+    ([12], 4096, "staged_ws_kernel<12, 15, 1, 1, 256, 1>"),
+    ([13], 4096, "staged_ws_kernel<12, 14, 1, 1, 256, 1>"),
+    ([15], 1 << 20, "staged_ws_kernel<12, 14, 1, 1, 512, 1>"),
+    ([12], 1 << 20, "staged_ws_kernel<12, 15, 1, 1, 512, 1>"),
+    ([0, 13], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1>"),
 ]
 
 

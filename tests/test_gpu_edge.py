@@ -112,15 +112,11 @@ def test_cpp_port_under_host_asan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.fixture(params=["staged", "staged_ws_late_gf", "staged_early", "staged_late", "staged_late_rt",
-                        "stepwise"])
+@pytest.fixture(params=["staged", "staged_early", "staged_late", "staged_late_rt", "stepwise"])
 def reconst_mode(request, monkeypatch):
     monkeypatch.delenv("XRS_RECONST", raising=False)
     monkeypatch.delenv("XRS_STAGED_LATE", raising=False)
     monkeypatch.delenv("XRS_STAGED_CT", raising=False)
-    monkeypatch.delenv("XRS_WS_EARLYB", raising=False)
-    if request.param == "staged_ws_late_gf":  # wave-specialised, stage 3 after the barrier
-        monkeypatch.setenv("XRS_WS_EARLYB", "0")
     if request.param == "staged_early":
         monkeypatch.setenv("XRS_STAGED_LATE", "0")
     elif request.param == "staged_late":  # compile-time kernel where it applies
@@ -204,8 +200,8 @@ def test_reconst_every_loss_pattern(rng, reconst_mode, order):
                 assert np.array_equal(a[i], b[i]), (lost, order, i)
 
 
-@pytest.mark.parametrize("ct", ["1", "1_lategf", "0", "0_onewave", "early", "late", "ws128", "ws256",
-                                "ws512", "ws512_lategf", "ws128o5"])
+@pytest.mark.parametrize("ct", ["1", "0", "0_onewave", "early", "late", "ws128", "ws256", "ws512",
+                                "ws128o5"])
 @pytest.mark.parametrize("size,n", [(4096, 600), (1 << 20, 4), (4112, 520)])
 def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     """General Reconst of batches large enough for the bandwidth kernels
@@ -214,10 +210,6 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("XRS_STAGED_CT", "0" if ct.startswith("0") else "1")
     monkeypatch.delenv("XRS_STAGED_WS", raising=False)
-    monkeypatch.delenv("XRS_WS_EARLYB", raising=False)
-    if ct.endswith("_lategf"):  # wave-specialised, stage 3 after the barrier
-        monkeypatch.setenv("XRS_WS_EARLYB", "0")
-        ct = ct[: -len("_lategf")]
     if ct == "0_onewave":  # the runtime-count one-wave late kernel
         monkeypatch.setenv("XRS_STAGED_WS", "0")
     if ct == "0":  # the runtime-count wave-specialised kernel

@@ -474,10 +474,6 @@ struct StagedArgs {
   uint32_t nmask[kStOut];
   uint32_t rmask[kStOut];  // the nonzero bret[] entries, compacted (late variant)
   int rb[kStOut];          // ... and their b-row indexes
-  // early-b wave-specialised kernels: stage-3 tables of the retrieveRS rows
-  // that are GF sources (rb[r] < nd: bit r of rgf), rt[r][u] = bt[rb[r]][u]
-  GfTab rt[kStOut][NN > 0 ? NN : 1];
-  uint32_t rgf;
   uint32_t bstore;
   int nd, na, nb, nl, nn, nr;
   BlockOrder order;
@@ -765,14 +761,7 @@ __global__ __launch_bounds__(BS) void staged_ct_kernel(const StagedArgs<NL, NN, 
 // pays one memory round trip, as Encode does, and holds only its own rows
 // (the one-wave-does-both kernels pay two round trips, or hold every row at
 // once at 144-161 VGPRs).
-// EB ("early b"): the b-lanes run stage 3's GF sum over their raw b-rows
-// BEFORE the barrier, in parallel with the a-lanes' stage 1, instead of
-// after it.  Stage 3 reads the b-rows in RS form (after retrieveRS), and GF
-// arithmetic is linear: sum_m bt[m] (b_m ^ rx_m) = sum_m bt[m] b_m ^
-// sum_m bt[m] rx_m, so the a-lanes fold the second sum (the retrieveRS rows
-// among the nd GF sources, tables rt[][], bits rgf) into the seeds they pass
-// through LDS, and after the barrier the b-lanes only XOR and store.
-template <int ND, int NB, int NL, int NN, int T, int OCC = 1, bool EB = true>
+template <int ND, int NB, int NL, int NN, int T, int OCC = 1>
 __global__ __launch_bounds__(2 * T) __attribute__((amdgpu_waves_per_eu(OCC)))
 void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   constexpr int W = 4;
@@ -783,7 +772,7 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   const bool valid = gid < a.total;
   const uint64_t stripe = gid / a.chunks;
   const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  uint32_t xb[NB][W], ob[NN][W];
+  uint32_t xb[NB][W];
   if (!blane) {
     if (valid) {
       uint32_t xa[ND][W], al[NL][W];
@@ -800,25 +789,17 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
       for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NL, W>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
       if constexpr (ND & 1) rows_mac1<NL, W>(al, a.at[ND - 1], xa[ND - 1]);
       // XOR terms of stage 2 (retrieveRS, xrs.go:305-320) and stage 4
-      // (re-piggyback, :281-297) for the b-lanes; EB: plus stage 3's GF sum
-      // over the retrieveRS terms of GF-source rows.
-      uint32_t corr[NN][W];
-#pragma unroll
-      for (int u = 0; u < NN; ++u)
-#pragma unroll
-        for (int w = 0; w < W; ++w) corr[u][w] = 0u;
+      // (re-piggyback, :281-297) for the b-lanes.
 #pragma unroll
       for (int r = 0; r < kStOut; ++r)
         if (r < a.nr) {
           uint32_t v[W] = {0u, 0u, 0u, 0u};
           abar_ct<ND, NL, W>(v, a.rmask[r], xa, al);
           xfer[r][t] = make_uint4(v[0], v[1], v[2], v[3]);
-          if constexpr (EB)
-            if ((a.rgf >> r) & 1u) rows_mac1<NN, W>(corr, a.rt[r], v);
         }
 #pragma unroll
       for (int u = 0; u < NN; ++u) {
-        uint32_t v[W] = {corr[u][0], corr[u][1], corr[u][2], corr[u][3]};
+        uint32_t v[W] = {0u, 0u, 0u, 0u};
         if (a.nmask[u]) abar_ct<ND, NL, W>(v, a.nmask[u], xa, al);
         xfer[kStOut + u][t] = make_uint4(v[0], v[1], v[2], v[3]);
       }
@@ -830,16 +811,6 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
 #pragma unroll
     for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (EB) {
-      // Stage 3 over the raw b-rows (xrs.go:270-275), overlapping stage 1.
-#pragma unroll
-      for (int u = 0; u < NN; ++u)
-#pragma unroll
-        for (int w = 0; w < W; ++w) ob[u][w] = 0u;
-#pragma unroll
-      for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
-      if constexpr (ND & 1) rows_mac1<NN, W>(ob, a.bt[ND - 1], xb[ND - 1]);
-    }
   }
   // LDS only: the b-lanes' row loads stay in flight across the barrier.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -857,27 +828,19 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
         xb[m][2] ^= v.z;
         xb[m][3] ^= v.w;
       }
+  uint32_t ob[NN][W];
 #pragma unroll
   for (int u = 0; u < NN; ++u) {
     const uint4 v = xfer[kStOut + u][t];
-    if constexpr (EB) {
-      ob[u][0] ^= v.x;
-      ob[u][1] ^= v.y;
-      ob[u][2] ^= v.z;
-      ob[u][3] ^= v.w;
-    } else {
-      ob[u][0] = v.x;
-      ob[u][1] = v.y;
-      ob[u][2] = v.z;
-      ob[u][3] = v.w;
-    }
+    ob[u][0] = v.x;
+    ob[u][1] = v.y;
+    ob[u][2] = v.z;
+    ob[u][3] = v.w;
   }
-  if constexpr (!EB) {
-    // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
+  // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
 #pragma unroll
-    for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
-    if constexpr (ND & 1) rows_mac1<NN, W>(ob, a.bt[ND - 1], xb[ND - 1]);
-  }
+  for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NN, W>(ob, a.bt[m], a.bt[m + 1], xb[m], xb[m + 1]);
+  if constexpr (ND & 1) rows_mac1<NN, W>(ob, a.bt[ND - 1], xb[ND - 1]);
 #pragma unroll
   for (int m = 0; m < NB; ++m)
     if ((a.bstore >> m) & 1u) stw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
@@ -1169,9 +1132,8 @@ int env_block(const char* var, int def) {
 }
 
 // Wave-specialised staged kernel: T chunks per block of 2*T lanes.
-// XRS_WS_EARLYB=0: stage 3 after the barrier (the round-2 form; A/B only).
-template <int NL, int NN, int T, int OCC = 1, bool EB = true>
-int launch_staged_ws_e(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+template <int NL, int NN, int T, int OCC = 1>
+int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + T - 1) / T;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
@@ -1183,51 +1145,34 @@ int launch_staged_ws_e(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStrea
   if constexpr (NL == 1) {
     // one lost parity vect (12+4: P12 -> nb = 15, P13..15 -> nb = 14)
     if (p.nb == 15) {
-      XRS_LAUNCH((staged_ws_kernel<12, 15, NL, NN, T, OCC, EB>), g, dim3(2 * T), stream, a);
+      XRS_LAUNCH((staged_ws_kernel<12, 15, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }
   if (p.nb == 12)
-    XRS_LAUNCH((staged_ws_kernel<12, 12, NL, NN, T, OCC, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 12, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   else if (p.nb == 13)
-    XRS_LAUNCH((staged_ws_kernel<12, 13, NL, NN, T, OCC, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 13, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   else
-    XRS_LAUNCH((staged_ws_kernel<12, 14, NL, NN, T, OCC, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<12, 14, NL, NN, T, OCC>), g, dim3(2 * T), stream, a);
   return static_cast<int>(hipGetLastError());
-}
-
-bool ws_early_b() {
-  const char* e = std::getenv("XRS_WS_EARLYB");
-  return !(e && e[0] == '0');
-}
-
-template <int NL, int NN, int T, int OCC = 1>
-int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
-  return ws_early_b() ? launch_staged_ws_e<NL, NN, T, OCC, true>(a, p, stream)
-                      : launch_staged_ws_e<NL, NN, T, OCC, false>(a, p, stream);
 }
 
 // Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
 // surviving piggybacked parity past dpHas[:d]), 256 chunks per block.
-template <int ND, int NL, int NN, int T = 256, bool EB = true>
-int launch_staged_ws_nd_e(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+template <int ND, int NL, int NN, int T = 256>
+int launch_staged_ws_nd(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + T - 1) / T;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kStaged, true, p.half, blocks, T);
   const dim3 g(static_cast<unsigned>(blocks));
   if (p.nb == ND)
-    XRS_LAUNCH((staged_ws_kernel<ND, ND, NL, NN, T, 1, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND, NL, NN, T>), g, dim3(2 * T), stream, a);
   else if (p.nb == ND + 1)
-    XRS_LAUNCH((staged_ws_kernel<ND, ND + 1, NL, NN, T, 1, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND + 1, NL, NN, T>), g, dim3(2 * T), stream, a);
   else
-    XRS_LAUNCH((staged_ws_kernel<ND, ND + 2, NL, NN, T, 1, EB>), g, dim3(2 * T), stream, a);
+    XRS_LAUNCH((staged_ws_kernel<ND, ND + 2, NL, NN, T>), g, dim3(2 * T), stream, a);
   return static_cast<int>(hipGetLastError());
-}
-
-template <int ND, int NL, int NN, int T = 256>
-int launch_staged_ws_nd(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
-  return ws_early_b() ? launch_staged_ws_nd_e<ND, NL, NN, T, true>(a, p, stream)
-                      : launch_staged_ws_nd_e<ND, NL, NN, T, false>(a, p, stream);
 }
 
 // NPRE < 0: every b-row early (NPRE = NB).
@@ -1275,10 +1220,6 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       break;
     }
     a.rb[a.nr] = m;
-    if (m < p.nd && m < kStSrc) {
-      a.rgf |= 1u << a.nr;
-      for (int u = 0; u < NN; ++u) a.rt[a.nr][u] = gf.tab(p.bcoef[m][u]);
-    }
     a.rmask[a.nr++] = p.bret[m];
   }
   a.nd = p.nd;

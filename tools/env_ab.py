@@ -60,9 +60,19 @@ def main():
         raise SystemExit(f"unknown CASE {case}")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t = {v: [] for v in vals}
+    # VAR=MULTI: each value sets several variables, "K1=V1+K2=V2" ("" = all
+    # of them unset); every variable any value names is unset first
+    multi_keys = sorted({kv.split("=")[0] for v in vals for kv in v.split("+") if kv}) \
+        if var == "MULTI" else []
     for _ in range(rounds):
         for v in vals:
-            if v:
+            if var == "MULTI":
+                for k in multi_keys:
+                    os.environ.pop(k, None)
+                for kv in (v.split("+") if v else []):
+                    k, _, val = kv.partition("=")
+                    os.environ[k] = val
+            elif v:
                 os.environ[var] = v
             else:  # an empty value = the library's default (variable unset)
                 os.environ.pop(var, None)

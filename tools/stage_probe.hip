@@ -155,6 +155,50 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  const bool sweep = argc > 3 && std::strcmp(argv[3], "sweep") == 0;
+  if (sweep) {
+    // staged pattern only: wave-specialised shape, T = 256 / 512 x block order K
+    for (uint64_t S : {uint64_t(1) << 20, uint64_t(256) << 10, uint64_t(4096)}) {
+      const uint64_t H = S / 2, stripe = 16 * S, n = total_bytes / stripe;
+      Args a;
+      std::memset(&a, 0, sizeof a);
+      for (int i = 2; i < 14; ++i) a.p.rd[i - 2] = uint64_t(i) * S;
+      for (int i = 2; i < 16; ++i) a.p.rd[12 + i - 2] = uint64_t(i) * S + H;
+      const uint64_t wr[7] = {0, S, H, S + H, 13 * S + H, 14 * S + H, 15 * S + H};
+      for (int w = 0; w < 7; ++w) a.p.wr[w] = wr[w];
+      a.base = reinterpret_cast<uint64_t>(buf);
+      a.scratch = reinterpret_cast<uint64_t>(scr);
+      a.stripe = stripe;
+      a.half = H;
+      a.chunks = H / 16;
+      a.total = a.chunks * n;
+      for (int T : {256, 512}) {
+        const uint64_t blocks = a.total / T;
+        for (uint32_t k : {0u, 1u, 2u, 4u, 8u, 16u, 32u, 64u, 128u, 256u}) {
+          a.nblk = static_cast<uint32_t>(blocks);
+          a.k = k;
+          auto launch = [&] {
+            if (T == 256) ws_kernel<12, 26, 2, 7, 256><<<blocks, 512>>>(a);
+            else ws_kernel<12, 26, 2, 7, 512><<<blocks, 1024>>>(a);
+          };
+          for (int i = 0; i < 3; ++i) launch();
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(e0));
+          for (int i = 0; i < reps; ++i) launch();
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          CK(hipGetLastError());
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          const double gbs = 33.0 * H * n / (ms / reps / 1e3) / 1e9;
+          std::printf("sweep S=%7llu ws%d k=%3u  %8.1f GB/s  %.3f of 8 TB/s\n", (unsigned long long)S, T, k,
+                      gbs, gbs / 8000.0);
+          std::fflush(stdout);
+        }
+      }
+    }
+    return 0;
+  }
   for (uint64_t S : {uint64_t(4096), uint64_t(65536), uint64_t(1) << 20}) {
     const uint64_t H = S / 2, stripe = 16 * S, n = total_bytes / stripe;
     auto A = [&](int shard) { return uint64_t(shard) * S; };

@@ -102,13 +102,25 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def _cpu_rates(o, seconds: float, threads: int):
-    """Bytes/s of the oracle's batch path on `threads` for the four bench
-    kernels and BASELINE config 4 (Update, Replace(4) @ 8 MiB), each run for
-    seconds/6 on a bounded sample."""
+def _cpu_samples():
+    """The CPU baseline's bounded sample, made once: 12+4 stripes of 4 KiB
+    (16,384 = 1 GiB) and 1 MiB (64 = 1 GiB); config 4: 16 stripes of [old,
+    new, 4 parity] (768 MiB) and of [4 data, 4 parity] (1 GiB) @ 8 MiB."""
     import numpy as np
 
     rng = np.random.Generator(np.random.PCG64(1))
+    return {
+        "4k": rng.integers(0, 256, size=(16384, D + P, ENC_S), dtype=np.uint8),
+        "1m": rng.integers(0, 256, size=(64, D + P, REC_S), dtype=np.uint8),
+        "upd": rng.integers(0, 256, size=(C4_STRIPES, 2 + P, C4_S), dtype=np.uint8),
+        "rep": rng.integers(0, 256, size=(C4_STRIPES, len(C4_ROWS) + P, C4_S), dtype=np.uint8),
+    }
+
+
+def _cpu_rates(o, seconds: float, threads: int, bufs: dict):
+    """Bytes/s of the oracle's batch path on `threads` for the four bench
+    kernels and BASELINE config 4 (Update, Replace(4) @ 8 MiB), each run for
+    seconds/6 on the bounded sample `bufs` (_cpu_samples)."""
 
     def run(fn, nbytes):
         fn(0)  # warm
@@ -121,23 +133,19 @@ def _cpu_rates(o, seconds: float, threads: int):
         return reps * nbytes / (time.perf_counter() - t0)
 
     rates = {}
-    for key, size, n in (("4k", ENC_S, 16384), ("1m", REC_S, 64)):  # 1 GiB each (> LLC)
-        buf = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+    for key, size in (("4k", ENC_S), ("1m", REC_S)):
+        buf = bufs[key]
+        n = buf.shape[0]
         rates["encode_" + key] = run(lambda i: o.encode_batch(buf, size, n, threads),
                                      n * (D + P) * size)
         rates["reconst_one_" + key] = run(
             lambda i: o.reconst_one_batch(buf, size, n, i % D, threads), n * 9 * size)
-        del buf
-    # config 4: 16 stripes of [old, new, 4 parity] (768 MiB) and of [4 data,
-    # 4 parity] (1 GiB) @ 8 MiB; bytes (2p+2)*S and (n+2p)*S per stripe
-    buf = rng.integers(0, 256, size=(C4_STRIPES, 2 + P, C4_S), dtype=np.uint8)
-    rates["update_8m"] = run(lambda i: o.update_batch(buf, C4_S, C4_STRIPES, i % D, threads),
+    # config 4: bytes (2p+2)*S and (n+2p)*S per stripe (xrs_test.go:600-680)
+    rates["update_8m"] = run(lambda i: o.update_batch(bufs["upd"], C4_S, C4_STRIPES, i % D, threads),
                              C4_STRIPES * (2 * P + 2) * C4_S)
-    del buf
-    buf = rng.integers(0, 256, size=(C4_STRIPES, len(C4_ROWS) + P, C4_S), dtype=np.uint8)
-    rates["replace4_8m"] = run(lambda i: o.replace_batch(buf, C4_S, C4_STRIPES, C4_ROWS, threads),
-                               C4_STRIPES * (len(C4_ROWS) + 2 * P) * C4_S)
-    del buf
+    rates["replace4_8m"] = run(
+        lambda i: o.replace_batch(bufs["rep"], C4_S, C4_STRIPES, C4_ROWS, threads),
+        C4_STRIPES * (len(C4_ROWS) + 2 * P) * C4_S)
     return rates
 
 
@@ -174,14 +182,15 @@ def cpu_baseline(seconds: float, step_bytes: dict):
         return sum(step_bytes.values()) / t_step / GIB
 
     counts = _cpu_counts()
-    r1 = _cpu_rates(o, seconds, 1)
+    bufs = _cpu_samples()
+    r1 = _cpu_rates(o, seconds, 1, bufs)
     tcounts = [counts["affinity"]]
     q = counts["cgroup_quota_cpus"]
     if q and int(q) >= 1 and int(q) < counts["affinity"]:
         tcounts.append(int(q))
     multi = []
     for t in tcounts:
-        rn = _cpu_rates(o, seconds / 2, t)
+        rn = _cpu_rates(o, seconds / 2, t, bufs)
         multi.append({"threads": t, "value": round(mix(rn), 3),
                       "gibps": {k: round(v / GIB, 3) for k, v in rn.items()}})
     best = max(multi, key=lambda m: m["value"])

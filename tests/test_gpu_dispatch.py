@@ -24,6 +24,15 @@ def _traced(fn):
     return list(xrs_amd.traced_kernels())
 
 
+def test_library_is_this_tree():
+    """The library these GPU tests load was built from this tree's sources:
+    xrs_version() carries the source digest (xrs_amd/csrc/version.cpp), the
+    tree's digest is recomputed here (xrs_amd.source_hash)."""
+    built, tree = xrs_amd.library_source_hash(), xrs_amd.source_hash()
+    print(f"library {xrs_amd.version()}, tree sources {tree}")
+    assert built == tree, f"stale library: built from {built}, tree is {tree}"
+
+
 @pytest.fixture(scope="module")
 def codec():
     return xrs_amd.XRS(D, P), OracleXRS(D, P)

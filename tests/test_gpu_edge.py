@@ -201,7 +201,7 @@ def test_reconst_every_loss_pattern(rng, reconst_mode, order):
 
 
 @pytest.mark.parametrize("ct", ["1", "0", "0_onewave", "early", "late", "ws128", "ws256", "ws512",
-                                "ws128o5", "glds"])
+                                "ws128o5"])
 @pytest.mark.parametrize("size,n", [(4096, 600), (1 << 20, 4), (4112, 520)])
 def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     """General Reconst of batches large enough for the bandwidth kernels
@@ -210,9 +210,6 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("XRS_STAGED_CT", "0" if ct.startswith("0") else "1")
     monkeypatch.delenv("XRS_STAGED_WS", raising=False)
-    monkeypatch.delenv("XRS_STAGED_GLDS", raising=False)
-    if ct == "glds":  # the LDS-DMA staged kernel
-        monkeypatch.setenv("XRS_STAGED_GLDS", "1")
     if ct == "0_onewave":  # the runtime-count one-wave late kernel
         monkeypatch.setenv("XRS_STAGED_WS", "0")
     if ct == "0":  # the runtime-count wave-specialised kernel

@@ -93,7 +93,6 @@ def test_kernel_register_budgets(tmp_path):
     # (26-27 rows; the launcher takes 1024-thread blocks only up to 22 rows,
     # XRS_ROWS_BLOCK=1024 forces them).
     ab_only = re.compile(r"staged_ws_kernelILi12ELi1[234]ELi[34]ELi[34]ELi128ELi5E|"
-                         r"staged_glds_kernelILi12ELi14ELi4ELi4E|"
                          r"rows_kernelILi2ELi20ELi[67]ELb0ELb1ELi1024E")
     spills = {s: v for s, v in ks.items() if v["scratch"] and not ab_only.search(s)}
     assert not spills, list(spills)[:5]

@@ -18,7 +18,7 @@ if [[ $STEPS == *ab* ]]; then
   ab() { echo "== $*" >> $out; env "$@" timeout -k 10 150 python tools/env_ab.py >> $out 2>&1 || { echo "rc=$?"; tail -5 $out; exit 1; }; }
   for size in 1048576 262144 4096; do
     for c in reconst_2 reconst_4 mixed_13 mixed_0-13; do
-      ab VAR=XRS_STAGED_GLDS VALS=,1 CASE=$c SIZE=$size ROUNDS=15
+      ab VAR=XRS_STAGED_GLDS VALS=,1,18 CASE=$c SIZE=$size ROUNDS=11
     done
   done
   grep -v amdgpu.ids $out

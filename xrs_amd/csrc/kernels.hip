@@ -848,142 +848,6 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
 }
 
-// LDS-DMA staged kernel (12+4 clean patterns, ND + NB rows per stripe, even):
-// one 256-lane block per CU, persistent, walks tiles of 128 chunks (2 KiB of
-// every half-row).  Each wave loads its share of a tile's rows straight into
-// LDS with global_load_lds_dwordx4 (no VGPR holds a row in flight), two tiles
-// ahead, into a ring of three slots; every lane then runs stages 1-4 for its
-// 8 bytes of the tile from LDS (ds_read_b64) and stores the outputs.  So
-// loads of the next two tiles stream while the GF work of this one runs,
-// which the one-pass kernels cannot do at one block per CU.
-//
-// The DMA is issued by inline asm (M0 holds the wave's LDS destination), so
-// the compiler's wait bookkeeping never sees it and never drains it early;
-// the kernel counts it itself.  Vector memory loads complete in order, so
-// with tile j+1's G DMAs issued after tile j's, "vmcnt <= G" means tile j's
-// have landed (this wave's; the barrier after the wait covers the others).
-__device__ __forceinline__ void glds16(const gu8* src, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_dst)
-      : "memory");
-}
-
-template <int G>
-__device__ __forceinline__ void wait_tile(bool next_in_flight) {
-  if (next_in_flight)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-constexpr int kGldsTile = 128;       // chunks (16 B) per tile: 2 KiB of each row
-constexpr int kGldsRowBytes = 2048;
-constexpr int kGldsSlots = 3;
-
-template <int ND, int NB, int NL, int NN, int NR>
-__global__ __launch_bounds__(256) void staged_glds_kernel(const StagedArgs<NL, NN, true> a) {
-  constexpr int R = ND + NB;
-  static_assert(R % 2 == 0, "two DMAs per row, four waves: an even row count");
-  constexpr int SLOT = R * kGldsRowBytes;
-  constexpr int G = R / 2;  // DMA instructions per wave per tile
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kGldsSlots * SLOT];
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t lds0 = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(lds)));
-  // persistent tiles: XCD-contiguous logical block, then a stride of the grid
-  const uint32_t nb = gridDim.x, b = blockIdx.x;
-  const uint32_t lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
-  const uint64_t tiles = a.total / kGldsTile;
-  const uint64_t ntiles = lb < tiles ? (tiles - lb + nb - 1) / nb : 0;
-  auto row_of = [&](int r) -> const RowRef& { return r < ND ? a.asrc[r] : a.bsrc[r - ND]; };
-  // this wave's DMAs for tile index t (of this block) into ring slot s:
-  // instruction i = 4k + wave, row i / 2, half i % 2 (1 KiB each)
-  auto issue = [&](uint64_t t, int s) {
-    const uint64_t tile = lb + t * nb;
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-      const int i = 4 * k + static_cast<int>(wave);
-      const int r = i >> 1, h = i & 1;
-      const uint64_t c = tile * kGldsTile + h * 64 + lane;
-      const uint64_t st = c / a.chunks;
-      const uint64_t off = a.off0 + (c - st * a.chunks) * 16;
-      const RowRef& rr = row_of(r);
-      glds16(reinterpret_cast<const gu8*>(rr.ptr + st * rr.stripe_stride + off),
-             lds0 + static_cast<uint32_t>(s * SLOT + r * kGldsRowBytes + h * 1024));
-    }
-  };
-  if (ntiles > 0) issue(0, 0);
-  if (ntiles > 1) issue(1, 1);
-  // this lane's 8 bytes of a tile: chunk t / 2, bytes (t % 2) * 8
-  const uint32_t t8 = threadIdx.x * 8;
-  for (uint64_t j = 0; j < ntiles; ++j) {
-    wait_tile<G>(j + 1 < ntiles);
-    __builtin_amdgcn_s_barrier();
-    if (j + 2 < ntiles) issue(j + 2, static_cast<int>((j + 2) % kGldsSlots));
-    const uint8_t* sl = lds + (j % kGldsSlots) * SLOT;
-    const uint64_t tile = lb + j * nb;
-    const uint64_t c = tile * kGldsTile + (threadIdx.x >> 1);
-    const uint64_t st = c / a.chunks;
-    const uint64_t off = a.off0 + (c - st * a.chunks) * 16 + (threadIdx.x & 1) * 8;
-    auto ldsrow = [&](uint32_t* v, int r) {
-      const uint2 x = *reinterpret_cast<const uint2*>(sl + r * kGldsRowBytes + t8);
-      v[0] = x.x;
-      v[1] = x.y;
-    };
-    // Stage 1: lost a-halves (xrs.go:247-262).
-    uint32_t xa[ND][2], al[NL][2];
-#pragma unroll
-    for (int m = 0; m < ND; ++m) ldsrow(xa[m], m);
-#pragma unroll
-    for (int q = 0; q < NL; ++q) al[q][0] = al[q][1] = 0u;
-#pragma unroll
-    for (int m = 0; m + 1 < ND; m += 2) rows_mac2<NL, 2>(al, a.at[m], a.at[m + 1], xa[m], xa[m + 1]);
-    if constexpr (ND & 1) rows_mac1<NL, 2>(al, a.at[ND - 1], xa[ND - 1]);
-    // XOR terms of stage 2 (retrieveRS, xrs.go:305-320) and stage 4
-    // (re-piggyback, :281-297).
-    uint32_t rx[NR][2], ob[NN][2];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      rx[r][0] = rx[r][1] = 0u;
-      abar_ct<ND, NL, 2>(rx[r], a.rmask[r], xa, al);
-    }
-#pragma unroll
-    for (int u = 0; u < NN; ++u) {
-      ob[u][0] = ob[u][1] = 0u;
-      if (a.nmask[u]) abar_ct<ND, NL, 2>(ob[u], a.nmask[u], xa, al);
-    }
-#pragma unroll
-    for (int q = 0; q < NL; ++q) stw<2>(al[q], row_addr(a.adst[q], st, off));
-    // Stages 2 and 3 over the b-rows (xrs.go:270-275), two at a time.
-#pragma unroll
-    for (int m = 0; m < NB; m += 2) {
-      uint32_t x0[2], x1[2];
-      ldsrow(x0, ND + m);
-      ldsrow(x1, ND + m + 1);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (a.rb[r] == m) x0[0] ^= rx[r][0], x0[1] ^= rx[r][1];
-        if (a.rb[r] == m + 1) x1[0] ^= rx[r][0], x1[1] ^= rx[r][1];
-      }
-      if ((a.bstore >> m) & 1u) stw<2>(x0, row_addr(a.bsrc[m], st, off));
-      if ((a.bstore >> (m + 1)) & 1u) stw<2>(x1, row_addr(a.bsrc[m + 1], st, off));
-      if (m + 1 < ND) rows_mac2<NN, 2>(ob, a.bt[m], a.bt[m + 1], x0, x1);
-      else if (m < ND) rows_mac1<NN, 2>(ob, a.bt[m], x0);
-    }
-#pragma unroll
-    for (int u = 0; u < NN; ++u) stw<2>(ob[u], row_addr(a.bdst[u], st, off));
-  }
-  // (every DMA this wave issued was waited for: the last tile waits vmcnt(0))
-}
-
 // Runtime-count form of staged_ws_kernel (any codec with d <= 16, lost parity
 // in the pattern, nl != nn): a-lanes load na a-rows, b-lanes nb b-rows, each
 // role's guarded loads issued together (each role waits once, so the
@@ -1294,32 +1158,6 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
   return static_cast<int>(hipGetLastError());
 }
 
-// LDS-DMA staged kernel (staged_glds_kernel): 12 a-rows, 12 or 14 b-rows
-// (an even row count), 2 or 3 retrieveRS rows, whole 128-chunk tiles; one
-// 256-lane block per CU.  kStagedDecline when the plan does not fit.
-template <int NL, int NN, int NB, int NR>
-int launch_staged_glds_t(const StagedArgs<NL, NN, true>& a, hipStream_t stream) {
-  const uint64_t tiles = a.total / kGldsTile;
-  const uint64_t blocks = std::min<uint64_t>(tiles, 256);
-  XRS_LAUNCH((staged_glds_kernel<12, NB, NL, NN, NR>), dim3(static_cast<unsigned>(blocks)), dim3(256),
-             stream, a);
-  return static_cast<int>(hipGetLastError());
-}
-
-template <int NL, int NN>
-int launch_staged_glds(const StagedArgs<NL, NN, true>& a, const StagedPlan& p, hipStream_t stream) {
-  const char* e = std::getenv("XRS_STAGED_GLDS");
-  if (!e || e[0] != '1') return kStagedDecline;
-  if (p.nd != 12 || p.na != 12 || a.total == 0 || a.total % kGldsTile) return kStagedDecline;
-  for (int m = 0; m < p.nb; ++m)  // every retrieveRS row written back (late form)
-    if (p.bret[m] && !((p.bstore >> m) & 1u)) return kStagedDecline;
-  if (p.nb == 14 && a.nr == 3) return launch_staged_glds_t<NL, NN, 14, 3>(a, stream);
-  if (p.nb == 14 && a.nr == 2) return launch_staged_glds_t<NL, NN, 14, 2>(a, stream);
-  if (p.nb == 12 && a.nr == 3) return launch_staged_glds_t<NL, NN, 12, 3>(a, stream);
-  if (p.nb == 12 && a.nr == 2) return launch_staged_glds_t<NL, NN, 12, 2>(a, stream);
-  return kStagedDecline;
-}
-
 // Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
 // surviving piggybacked parity past dpHas[:d]), 256 chunks per block.
 template <int ND, int NL, int NN, int T = 256>
@@ -1504,10 +1342,6 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // 2 lost from 512 KiB vects: 512 chunks per block (+1.2 / +2.3 / +4.2%
       // at 1 MiB / 512 KiB / 2 MiB vects over 256; at 256 KiB vects -4%).
       const char* wv = std::getenv("XRS_STAGED_WS");
-      {
-        const int rg = launch_staged_glds<NL, NN>(a, p, stream);
-        if (rg != kStagedDecline) return rg;
-      }
       if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {
         if (NL == 2 && p.half >= (256u << 10)) return launch_staged_ws<NL, NN, 512>(a, p, stream);
         if (NL <= 3) return launch_staged_ws<NL, NN, 256>(a, p, stream);
@@ -1532,8 +1366,6 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
     const bool ct1 = late && p.nd == 12 && p.na == 12 && p.nl == 1 && p.nn == 1 && p.nb >= 12 &&
                      p.nb <= 15 && !(cv && cv[0] == '0') && !(wv && *wv);
     if (ct1) {
-      const int rg = launch_staged_glds<1, 1>(a, p, stream);
-      if (rg != kStagedDecline) return rg;
       if (p.half >= (256u << 10)) return launch_staged_ws<1, 1, 512>(a, p, stream);
       return launch_staged_ws<1, 1, 256>(a, p, stream);
     }

@@ -594,30 +594,38 @@ def config4(R: Rank, args):
         return e0.elapsed_time(e1) / reps / 1e3
 
     for op, rows_per, n in (("update", 2 + P, n_upd), ("replace4", nr + P, n_rep)):
-        stripe = rows_per * S
+        # the library's recommended layout for rows_per vects of 8 MiB per
+        # stripe (xrs_batch_strides: a 4 KiB + 256 B pad per vect from 4 MiB)
+        sh, stripe = R.xrs_amd.batch_strides(S, rows_per)
         buf = R.random_bytes(n * stripe, 0xC04 + len(op))
         b = buf.data_ptr()
-        par = (2 if op == "update" else nr) * S  # parity offset in a stripe
+        par = (2 if op == "update" else nr) * sh  # parity offset in a stripe
         if op == "update":
-            fn = lambda i: x.update_batched(b, stripe, b + S, stripe, S, i % D, b + par, S, stripe, n, s)
+            fn = lambda i: x.update_batched(b, stripe, b + sh, stripe, S, i % D, b + par, sh, stripe, n, s)
             algo = n * (2 * P + 2) * S
         else:
-            fn = lambda i: x.replace_batched(b, S, stripe, list(C4_ROWS), S, b + par, S, stripe, n, s)
+            fn = lambda i: x.replace_batched(b, sh, stripe, list(C4_ROWS), S, b + par, sh, stripe, n, s)
             algo = n * (nr + 2 * P) * S
         sec = timed(fn, args.config4_steps)
         idx = [0, n - 1]
         view = buf.view(n, stripe)
         R.sync()
-        before = torch.stack([view[t].view(rows_per, S) for t in idx]).cpu().numpy()
+
+        def grab():
+            return torch.stack([torch.stack([view[t, i * sh:i * sh + S] for i in range(rows_per)])
+                                for t in idx]).cpu().numpy()
+
+        before = grab()
         row = 5
         if op == "update":
-            x.update_batched(b, stripe, b + S, stripe, S, row, b + par, S, stripe, n, s)
+            x.update_batched(b, stripe, b + sh, stripe, S, row, b + par, sh, stripe, n, s)
         else:
             fn(0)
         R.sync()
-        got = torch.stack([view[t].view(rows_per, S) for t in idx]).cpu().numpy()
+        got = grab()
         samples.append(("config4_" + op, op, row if op == "update" else -1, idx, before, got))
         out[op] = {"stripes": n, "bytes_per_launch": algo, "ms": round(sec * 1e3, 4),
+                   "shard_stride": sh, "stripe_stride": stripe,
                    "gibps": round(algo / sec / GIB, 1), "frac": round(algo / sec / 1e9 / HBM_PEAK_GBS, 4)}
         del buf, view
         torch.cuda.empty_cache()

@@ -30,8 +30,10 @@ if [[ $STEPS == *bench* ]]; then
   run bench 600 python bench.py ${BENCH_ARGS:-} || exit $?
 fi
 if [[ $STEPS == *prof* ]]; then
+  # 40 timed steps after a 2 s soak: the dominant launch's --stats average is
+  # then within a fraction of a percent of the line's HIP-event timing
   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config5-stripes 0 --host-mib 0 --ramp-seconds 0.5 \
-      --xgmi-stripes 0 || exit $?
+      python bench.py --steps 40 --warmup 2 --no-cpu-baseline --config5-stripes 0 --host-mib 0 --ramp-seconds 2 \
+      --xgmi-stripes 0 --config4-stripes 0 --queue-callers || exit $?
 fi
 exit 0

@@ -69,6 +69,8 @@ STAGED = [
     ([15], 1 << 20, "staged_ws_kernel<12, 14, 1, 1, 512, 1>"),
     ([12], 1 << 20, "staged_ws_kernel<12, 15, 1, 1, 512, 1>"),
     ([0, 13], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1>"),
+    ([0, 5], 1 << 20, "staged_wsp_kernel<12, 14, 2, 2, 512>"),
+    ([0, 5, 7], 1 << 20, "staged_ws_kernel<12, 13, 3, 3, 256, 1>"),
 ]
 
 

@@ -239,6 +239,92 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
             assert np.array_equal(got[st], np.stack(w)), (lost, need, st)
 
 
+@pytest.mark.parametrize("wsp,grid", [("512", ""), ("256", ""), ("512", "24"), ("256", "7"),
+                                      ("512", "1"), ("", ""), ("", "13")])
+@pytest.mark.parametrize("size,n", [(4096, 601), (1 << 20, 5)])
+def test_reconst_batched_persistent_vs_oracle(rng, monkeypatch, wsp, grid, size, n):
+    """The persistent wave-specialised kernel (staged_wsp_kernel; XRS_WSP
+    forces it for 2-4 lost, the default runs it for 2 lost from 256 to 768
+    KiB halves): every block takes several tiles from the launch's counter when
+    XRS_WSP_GRID caps the grid (ragged last tile, uneven tile counts per
+    block, both LDS slots reused), every stripe vs the oracle, side effects
+    included (xrs.go:236-320)."""
+    torch = pytest.importorskip("torch")
+    if wsp:
+        monkeypatch.setenv("XRS_WSP", wsp)
+    else:  # the default: the persistent kernel for 2 lost from 256-768 KiB halves only
+        monkeypatch.delenv("XRS_WSP", raising=False)
+    monkeypatch.delenv("XRS_STAGED_WS", raising=False)
+    monkeypatch.delenv("XRS_STAGED_CT", raising=False)
+    if grid:
+        monkeypatch.setenv("XRS_WSP_GRID", grid)
+    else:
+        monkeypatch.delenv("XRS_WSP_GRID", raising=False)
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    s = torch.cuda.current_stream().cuda_stream
+    for lost, need in (([0, 1], [0, 1]), ([0, 1, 2], [0, 1, 2]), ([0, 1, 2, 3], [0, 1, 2, 3]),
+                       ([4, 9], [9, 4]), ([2, 5, 11], [5])):
+        h = host.copy()
+        h[:, lost] = 0x5A
+        has = [i for i in range(D + P) if i not in lost]
+        t = torch.from_numpy(h).cuda()
+        xrs_amd.trace_kernels(True)
+        try:
+            x.reconst_batched(t.data_ptr(), size, size, (D + P) * size, n, has, need, s)
+            torch.cuda.synchronize()
+        finally:
+            xrs_amd.trace_kernels(False)
+        names = list(xrs_amd.traced_kernels())
+        persistent = [k for k in names if k.startswith("staged_wsp_kernel<12, ")]
+        if sorted(lost) == sorted(need) and (wsp or (len(lost) == 2 and 1 << 19 <= size <= 3 << 19)):
+            assert len(names) == 1 and persistent, names
+        elif not wsp:
+            assert not persistent, names
+        got = t.cpu().numpy()
+        for st in range(n):
+            w = [h[st, i].copy() for i in range(D + P)]
+            o.reconst(w, has, need)
+            assert np.array_equal(got[st], np.stack(w)), (lost, need, st)
+
+
+def test_reconst_persistent_concurrent_streams(rng, monkeypatch):
+    """Persistent 2-lost launches on four streams at once (each launch owns
+    its tile counter): every stripe of every batch vs the oracle."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.delenv("XRS_WSP", raising=False)
+    monkeypatch.setenv("XRS_WSP_GRID", "64")  # many tiles per block, long overlap
+    size, n = 1 << 20, 6
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    lost = [3, 8]
+    h = host.copy()
+    h[:, lost] = 0x5A
+    has = [i for i in range(D + P) if i not in lost]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    ts = [torch.from_numpy(h).cuda() for _ in streams]
+    torch.cuda.synchronize()
+    xrs_amd.trace_kernels(True)
+    try:
+        for t, st in zip(ts, streams):
+            x.reconst_batched(t.data_ptr(), size, size, (D + P) * size, n, has, lost, st.cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        xrs_amd.trace_kernels(False)
+    assert list(xrs_amd.traced_kernels()) == ["staged_wsp_kernel<12, 14, 2, 2, 512>"]
+    want = []
+    for st in range(n):
+        w = [h[st, i].copy() for i in range(D + P)]
+        o.reconst(w, has, lost)
+        want.append(np.stack(w))
+    for t in ts:
+        got = t.cpu().numpy()
+        for st in range(n):
+            assert np.array_equal(got[st], want[st]), st
+
+
 @pytest.mark.parametrize("ws", ["", "0", "rt"])
 @pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4), (15, 5), (8, 4), (14, 4),
                                  (10, 2)])

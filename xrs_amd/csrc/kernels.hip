@@ -145,13 +145,16 @@ struct BlockOrder {
   uint32_t k;     // logical blocks per XCD per group; 0: plain order
 };
 
-__device__ __forceinline__ uint64_t logical_block(const BlockOrder& o) {
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ uint64_t logical_of(const BlockOrder& o, uint32_t b) {
   if (o.k == 0) return b;
   const uint32_t q = b >> 3, g = q / o.k;
   const uint64_t span = 8ull * o.k;
   if ((g + 1) * span > o.nblk) return b;
   return g * span + (b & 7u) * static_cast<uint64_t>(o.k) + (q - g * o.k);
+}
+
+__device__ __forceinline__ uint64_t logical_block(const BlockOrder& o) {
+  return logical_of(o, blockIdx.x);
 }
 
 // ============================================================ pair kernel
@@ -848,6 +851,197 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
 }
 
+// Persistent form of staged_ws_kernel for 2 lost data vects from 256 to 768
+// KiB halves: one block of 2*T lanes per CU takes T-chunk tiles from a launch-wide
+// counter, as the hardware dispatcher hands out blocks (so the tiles in
+// flight stay a compact stretch of the batch), and the two roles run one tile
+// apart.  Per tile j: the a-lanes load tile j's a-rows, rebuild and store the
+// lost a-halves and leave the XOR terms in LDS slot j & 1, while lane 0 takes
+// tile j+1 from the counter into nexttile[(j+1) & 1]; one barrier; the
+// b-lanes, whose b-rows of tile j were issued before it, finish stages 2-4 of
+// tile j and issue tile j+1's b-rows, while the a-lanes are already loading
+// tile j+1.  Each role's GF work and stores overlap the other role's loads
+// and no block turnover sits between tiles.  Slot s is rewritten two tiles
+// later, after a barrier that the b-lanes reach only once they have read it.
+// Tile v is logical block v of the XCD order (K = the tiles of one
+// half-vect, so each XCD works through one stripe per group).
+//
+// Kernel-argument reads in the loops go through a pointer the compiler
+// cannot see through (kargs): each tile re-reads its tables and row refs
+// with scalar loads instead of hoisting all of them into SGPRs, which
+// spills.  (Taking the address of the by-value argument copies it to
+// scratch instead.)
+#define XRS_KC __attribute__((address_space(4)))
+template <class A>
+__device__ __forceinline__ const XRS_KC A* kargs() {
+  const XRS_KC A* p = (const XRS_KC A*)(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ GfTab kld(const XRS_KC GfTab& r) {
+  return GfTab{r.lo0, r.hi0, r.lo1, r.hi1, r.top};
+}
+__device__ __forceinline__ RowRef kld(const XRS_KC RowRef& r) { return RowRef{r.ptr, r.stripe_stride}; }
+__device__ __forceinline__ BlockOrder kld(const XRS_KC BlockOrder& r) { return BlockOrder{r.nblk, r.k}; }
+template <int R>
+__device__ __forceinline__ void ktabs(GfTab (&t)[R], const XRS_KC GfTab* src) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) t[r] = kld(src[r]);
+}
+
+template <int ND, int NB, int NL, int NN, int T>
+__global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, NN, true> a,
+                                                            const uint32_t ntiles, uint32_t* ctr) {
+  using Args = StagedArgs<NL, NN, true>;
+  constexpr int W = 4;
+  __shared__ uint4 xfer[2][kStOut + NN][T];
+  __shared__ uint32_t nexttile[2];
+  // Wave-uniform role (T is a multiple of 64): two separate loops, so neither
+  // role's rows are live while the other role's code runs.
+  const bool blane = __builtin_amdgcn_readfirstlane(threadIdx.x) >= T;
+  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
+  uint32_t v = blockIdx.x;  // each block's first tile; the rest from *ctr
+  if (!blane) {
+    for (uint32_t j = 0; v < ntiles; ++j) {
+      const XRS_KC Args* q = kargs<Args>();
+      const uint32_t s = j & 1u;
+      uint32_t nv = 0;
+      if (threadIdx.x == 0) nv = atomicAdd(ctr, 1u) + gridDim.x;
+      const uint64_t gid = logical_of(kld(q->order), v) * T + t;
+      if (gid < q->total) {
+        const uint64_t chunks = q->chunks;
+        const uint64_t stripe = gid / chunks;
+        const uint64_t off = q->off0 + (gid - stripe * chunks) * (4 * W);
+        uint32_t xa[ND][W], al[NL][W];
+#pragma unroll
+        for (int m = 0; m < ND; ++m) ldw<W>(xa[m], row_addr(kld(q->asrc[m]), stripe, off));
+        // Stage 1: lost a-halves (xrs.go:247-262).
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+#pragma unroll
+          for (int w = 0; w < W; ++w) al[l][w] = 0u;
+#pragma unroll
+        for (int m = 0; m + 1 < ND; m += 2) {
+          GfTab t0[NL], t1[NL];
+          ktabs<NL>(t0, q->at[m]);
+          ktabs<NL>(t1, q->at[m + 1]);
+          rows_mac2<NL, W>(al, t0, t1, xa[m], xa[m + 1]);
+        }
+        if constexpr (ND & 1) {
+          GfTab t0[NL];
+          ktabs<NL>(t0, q->at[ND - 1]);
+          rows_mac1<NL, W>(al, t0, xa[ND - 1]);
+        }
+        // XOR terms of stage 2 (retrieveRS, xrs.go:305-320) and stage 4
+        // (re-piggyback, :281-297) for the b-lanes.
+        const int nr = q->nr;
+#pragma unroll
+        for (int r = 0; r < kStOut; ++r)
+          if (r < nr) {
+            uint32_t x[W] = {0u, 0u, 0u, 0u};
+            abar_ct<ND, NL, W>(x, q->rmask[r], xa, al);
+            xfer[s][r][t] = make_uint4(x[0], x[1], x[2], x[3]);
+          }
+#pragma unroll
+        for (int u = 0; u < NN; ++u) {
+          uint32_t x[W] = {0u, 0u, 0u, 0u};
+          const uint32_t nm = q->nmask[u];
+          if (nm) abar_ct<ND, NL, W>(x, nm, xa, al);
+          xfer[s][kStOut + u][t] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+#pragma unroll
+        for (int l = 0; l < NL; ++l) stw<W>(al[l], row_addr(kld(q->adst[l]), stripe, off));
+      }
+      if (threadIdx.x == 0) nexttile[s ^ 1u] = nv;
+      // LDS only: no wait on this wave's stores at the barrier.
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      v = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
+    }
+    return;
+  }
+  uint32_t xb[NB][W];
+  if (v < ntiles) {
+    const uint64_t gid = logical_of(a.order, v) * T + t;
+    if (gid < a.total) {
+      const uint64_t stripe = gid / a.chunks;
+      const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+#pragma unroll
+      for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(a.bsrc[m], stripe, off));
+    }
+  }
+  for (uint32_t j = 0; v < ntiles; ++j) {
+    const XRS_KC Args* q = kargs<Args>();
+    const uint32_t s = j & 1u;
+    const BlockOrder order = kld(q->order);
+    const uint64_t total = q->total, chunks = q->chunks, off0 = q->off0;
+    const uint64_t gid = logical_of(order, v) * T + t;
+    // LDS only: this tile's b-row loads stay in flight across the barrier.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (gid < total) {
+      const uint64_t stripe = gid / chunks;
+      const uint64_t off = off0 + (gid - stripe * chunks) * (4 * W);
+      const int nr = q->nr;
+#pragma unroll
+      for (int r = 0; r < kStOut; ++r)
+        if (r < nr) {
+          const int rb = q->rb[r];
+          const uint4 x = xfer[s][r][t];
+#pragma unroll
+          for (int m = 0; m < NB; ++m)
+            if (rb == m) {
+              xb[m][0] ^= x.x;
+              xb[m][1] ^= x.y;
+              xb[m][2] ^= x.z;
+              xb[m][3] ^= x.w;
+            }
+        }
+      uint32_t ob[NN][W];
+#pragma unroll
+      for (int u = 0; u < NN; ++u) {
+        const uint4 x = xfer[s][kStOut + u][t];
+        ob[u][0] = x.x;
+        ob[u][1] = x.y;
+        ob[u][2] = x.z;
+        ob[u][3] = x.w;
+      }
+      // Stage 3: needed b-halves from the RS-form b-rows (xrs.go:270-275).
+#pragma unroll
+      for (int m = 0; m + 1 < ND; m += 2) {
+        GfTab t0[NN], t1[NN];
+        ktabs<NN>(t0, q->bt[m]);
+        ktabs<NN>(t1, q->bt[m + 1]);
+        rows_mac2<NN, W>(ob, t0, t1, xb[m], xb[m + 1]);
+      }
+      if constexpr (ND & 1) {
+        GfTab t0[NN];
+        ktabs<NN>(t0, q->bt[ND - 1]);
+        rows_mac1<NN, W>(ob, t0, xb[ND - 1]);
+      }
+      const uint32_t bstore = q->bstore;
+#pragma unroll
+      for (int m = 0; m < NB; ++m)
+        if ((bstore >> m) & 1u) stw<W>(xb[m], row_addr(kld(q->bsrc[m]), stripe, off));
+#pragma unroll
+      for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(kld(q->bdst[u]), stripe, off));
+    }
+    const uint32_t vn = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
+    if (vn < ntiles) {
+      const uint64_t gn = logical_of(order, vn) * T + t;
+      if (gn < total) {
+        const uint64_t sn = gn / chunks;
+        const uint64_t on = off0 + (gn - sn * chunks) * (4 * W);
+#pragma unroll
+        for (int m = 0; m < NB; ++m) ldw<W>(xb[m], row_addr(kld(q->bsrc[m]), sn, on));
+      }
+    }
+    v = vn;
+  }
+}
+
 // Runtime-count form of staged_ws_kernel (any codec with d <= 16, lost parity
 // in the pattern, nl != nn): a-lanes load na a-rows, b-lanes nb b-rows, each
 // role's guarded loads issued together (each role waits once, so the
@@ -1158,6 +1352,63 @@ int launch_staged_ws(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_
   return static_cast<int>(hipGetLastError());
 }
 
+// Compute units of the stream's device (cached per device).
+int cu_count(hipStream_t s) {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+// Persistent wave-specialised staged kernel (staged_wsp_kernel): one block
+// of 2*T lanes per compute unit (XRS_WSP_PER_CU: more, A/B; XRS_WSP_GRID: an
+// exact block count, so tests give every block many tiles), K = the tiles of
+// one half-vect (XRS_WS_ORDER overrides).  The tile counter is this launch's
+// own (stream-ordered allocation, so launches on other streams never share
+// it).  Returns kNotLaunched when it cannot be allocated; the caller then
+// runs the one-shot kernel.
+constexpr int kNotLaunched = -1;
+template <int NL, int NN, int T>
+int launch_staged_wsp(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
+  const uint64_t tiles = (a.total + T - 1) / T;
+  if (tiles > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kStaged, true, p.half, tiles, T);
+  a.order.k = static_cast<uint32_t>(std::max<uint64_t>(1, a.chunks / T));
+  if (const char* e = std::getenv("XRS_WS_ORDER")) {  // A/B knob
+    a.order.k = std::strcmp(e, "full") == 0 ? static_cast<uint32_t>(tiles / 8)
+                                            : static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+  }
+  uint64_t per_cu = 1;
+  if (const char* e = std::getenv("XRS_WSP_PER_CU")) per_cu = std::max<uint64_t>(1, std::strtoul(e, nullptr, 10));
+  uint64_t grid = per_cu * static_cast<uint64_t>(cu_count(stream));
+  if (const char* e = std::getenv("XRS_WSP_GRID")) grid = std::max<uint64_t>(1, std::strtoul(e, nullptr, 10));
+  grid = std::min<uint64_t>(tiles, grid);
+  const dim3 g(static_cast<unsigned>(grid));
+  const uint32_t nt = static_cast<uint32_t>(tiles);
+  uint32_t* ctr = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), stream) != hipSuccess) {
+    (void)hipGetLastError();
+    return kNotLaunched;
+  }
+  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), stream);
+  if (e == hipSuccess) {
+    if (p.nb == 12)
+      XRS_LAUNCH((staged_wsp_kernel<12, 12, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
+    else if (p.nb == 13)
+      XRS_LAUNCH((staged_wsp_kernel<12, 13, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
+    else
+      XRS_LAUNCH((staged_wsp_kernel<12, 14, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(ctr, stream);
+  return static_cast<int>(e != hipSuccess ? e : f);
+}
+
 // Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
 // surviving piggybacked parity past dpHas[:d]), 256 chunks per block.
 template <int ND, int NL, int NN, int T = 256>
@@ -1342,6 +1593,22 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // 2 lost from 512 KiB vects: 512 chunks per block (+1.2 / +2.3 / +4.2%
       // at 1 MiB / 512 KiB / 2 MiB vects over 256; at 256 KiB vects -4%).
       const char* wv = std::getenv("XRS_STAGED_WS");
+      // 2 lost from 256 to 768 KiB halves: the persistent form, 512 chunks
+      // per tile (bytes moved, interleaved medians vs the one-shot 512-chunk
+      // kernel, profiles/r04_wsp_ab.log: 512 KiB / 768 KiB / 1 MiB / 1.5 MiB
+      // vects +2.9 / -0.1 / +4.2 / +2.6%; 2 / 4 / 8 MiB -1.8 / +0.7 / -14.7%,
+      // so larger halves keep the one-shot kernel; 3 lost -2..-4% and
+      // 256-chunk tiles -5..-21%, profiles/r04_wsp_sizes.log).
+      // XRS_WSP=0 turns it off, =512 / =256 forces it (A/B, tests).
+      const char* pv = std::getenv("XRS_WSP");
+      const bool wsp_off = pv && pv[0] == '0';
+      int wsp = kNotLaunched;
+      if (pv && std::strcmp(pv, "256") == 0) wsp = launch_staged_wsp<NL, NN, 256>(a, p, stream);
+      else if (pv && std::strcmp(pv, "512") == 0) wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
+      else if (NL == 2 && !wsp_off && (!wv || !*wv || std::strcmp(wv, "rt") == 0) &&
+               p.half >= (256u << 10) && p.half <= (768u << 10))
+        wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
+      if (wsp != kNotLaunched) return wsp;
       if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {
         if (NL == 2 && p.half >= (256u << 10)) return launch_staged_ws<NL, NN, 512>(a, p, stream);
         if (NL <= 3) return launch_staged_ws<NL, NN, 256>(a, p, stream);

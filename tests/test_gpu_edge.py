@@ -245,14 +245,14 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
 def test_reconst_batched_persistent_vs_oracle(rng, monkeypatch, wsp, grid, size, n):
     """The persistent wave-specialised kernel (staged_wsp_kernel; XRS_WSP
     forces it for 2-4 lost, the default runs it for 2 lost from 256 to 768
-    KiB halves): every block takes several tiles from the launch's counter when
+    KiB halves in launches of at least 16 tiles per CU, test_gpu_dispatch.py): every block takes several tiles from the launch's counter when
     XRS_WSP_GRID caps the grid (ragged last tile, uneven tile counts per
     block, both LDS slots reused), every stripe vs the oracle, side effects
     included (xrs.go:236-320)."""
     torch = pytest.importorskip("torch")
     if wsp:
         monkeypatch.setenv("XRS_WSP", wsp)
-    else:  # the default: the persistent kernel for 2 lost from 256-768 KiB halves only
+    else:  # the default: the persistent kernel only for large 2-lost launches
         monkeypatch.delenv("XRS_WSP", raising=False)
     monkeypatch.delenv("XRS_STAGED_WS", raising=False)
     monkeypatch.delenv("XRS_STAGED_CT", raising=False)
@@ -278,9 +278,9 @@ def test_reconst_batched_persistent_vs_oracle(rng, monkeypatch, wsp, grid, size,
             xrs_amd.trace_kernels(False)
         names = list(xrs_amd.traced_kernels())
         persistent = [k for k in names if k.startswith("staged_wsp_kernel<12, ")]
-        if sorted(lost) == sorted(need) and (wsp or (len(lost) == 2 and 1 << 19 <= size <= 3 << 19)):
+        if sorted(lost) == sorted(need) and wsp:
             assert len(names) == 1 and persistent, names
-        elif not wsp:
+        elif not wsp:  # these batches are under the default's size threshold
             assert not persistent, names
         got = t.cpu().numpy()
         for st in range(n):
@@ -293,7 +293,7 @@ def test_reconst_persistent_concurrent_streams(rng, monkeypatch):
     """Persistent 2-lost launches on four streams at once (each launch owns
     its tile counter): every stripe of every batch vs the oracle."""
     torch = pytest.importorskip("torch")
-    monkeypatch.delenv("XRS_WSP", raising=False)
+    monkeypatch.setenv("XRS_WSP", "512")
     monkeypatch.setenv("XRS_WSP_GRID", "64")  # many tiles per block, long overlap
     size, n = 1 << 20, 6
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)

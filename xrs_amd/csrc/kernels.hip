@@ -1373,6 +1373,40 @@ int cu_count(hipStream_t s) {
 // it).  Returns kNotLaunched when it cannot be allocated; the caller then
 // runs the one-shot kernel.
 constexpr int kNotLaunched = -1;
+
+// A memory pool of the library's own for those counters, keeping what it
+// reserves (release threshold: never), so a launch's counter costs no
+// driver allocation; nullptr (the device's default pool) if it cannot be made.
+hipMemPool_t counter_pool(hipStream_t s) {
+  static std::mutex mu;
+  static hipMemPool_t pools[64] = {};
+  static bool tried[64] = {};
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(mu);
+  if (!tried[dev]) {
+    tried[dev] = true;
+    hipMemPoolProps pp;
+    std::memset(&pp, 0, sizeof(pp));
+    pp.allocType = hipMemAllocationTypePinned;
+    pp.handleTypes = hipMemHandleTypeNone;
+    pp.location.type = hipMemLocationTypeDevice;
+    pp.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &pp) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      pools[dev] = pool;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  return pools[dev];
+}
+
 template <int NL, int NN, int T>
 int launch_staged_wsp(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream_t stream) {
   const uint64_t tiles = (a.total + T - 1) / T;
@@ -1391,7 +1425,11 @@ int launch_staged_wsp(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream
   const dim3 g(static_cast<unsigned>(grid));
   const uint32_t nt = static_cast<uint32_t>(tiles);
   uint32_t* ctr = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), stream) != hipSuccess) {
+  const hipMemPool_t pool = counter_pool(stream);
+  const hipError_t ae =
+      pool ? hipMallocFromPoolAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), pool, stream)
+           : hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), stream);
+  if (ae != hipSuccess) {
     (void)hipGetLastError();
     return kNotLaunched;
   }
@@ -1599,6 +1637,11 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // vects +2.9 / -0.1 / +4.2 / +2.6%; 2 / 4 / 8 MiB -1.8 / +0.7 / -14.7%,
       // so larger halves keep the one-shot kernel; 3 lost -2..-4% and
       // 256-chunk tiles -5..-21%, profiles/r04_wsp_sizes.log).
+      // Only launches of at least 16 tiles per CU (64 stripes of 1 MiB):
+      // the per-launch counter (alloc from counter_pool + memset + free)
+      // costs 2-7 us per synchronous call, which smaller launches do not win
+      // back (tools/wsp_call_overhead.py, profiles/r04_wsp_overhead.log:
+      // 4 / 16 / 64 / 256 stripes of 1 MiB +7.0 / +2.4 / -4.5 / -34 us).
       // XRS_WSP=0 turns it off, =512 / =256 forces it (A/B, tests).
       const char* pv = std::getenv("XRS_WSP");
       const bool wsp_off = pv && pv[0] == '0';
@@ -1606,7 +1649,8 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       if (pv && std::strcmp(pv, "256") == 0) wsp = launch_staged_wsp<NL, NN, 256>(a, p, stream);
       else if (pv && std::strcmp(pv, "512") == 0) wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
       else if (NL == 2 && !wsp_off && (!wv || !*wv || std::strcmp(wv, "rt") == 0) &&
-               p.half >= (256u << 10) && p.half <= (768u << 10))
+               p.half >= (256u << 10) && p.half <= (768u << 10) &&
+               a.total >= uint64_t(512) * 16 * static_cast<uint64_t>(cu_count(stream)))
         wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
       if (wsp != kNotLaunched) return wsp;
       if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {

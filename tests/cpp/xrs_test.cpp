@@ -405,6 +405,64 @@ static void TestQueue_Oversubscribed() {
   if (bad) FATAL("%d mismatches or errors", bad.load());
 }
 
+// Not in the reference: the persistent staged kernel forced for every
+// 2-lost launch (XRS_WSP=512; by default it runs only for large batches), on
+// an 8-block grid so each block takes many tiles from its launch's counter,
+// from 8 threads on one codec: counters come from the library's
+// stream-ordered pool while other launches hold theirs.  Host-resident
+// batches of 4 stripes of 1 MiB vects in pinned, mapped memory (the kernels
+// run in place over PCIe).  The rebuilt data vects must equal the encoded
+// ones (the surviving parity's b-halves come back in RS form, the
+// reference's retrieveRS side effect, so parity is not compared).
+static void TestXRS_ReconstPersistent() {
+  setenv("XRS_WSP", "512", 1);
+  setenv("XRS_WSP_GRID", "8", 1);
+  auto x = must_new(kData, kParity);
+  xrs_trace_kernels(1);
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  constexpr size_t S = 1 << 20, n = 4, stripe = (kData + kParity) * S;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937_64 r(700 + t);
+      uint8_t* h = static_cast<uint8_t*>(xrs_host_alloc(n * stripe));
+      if (!h) {
+        ++bad;
+        return;
+      }
+      for (int i = 0; i < 3; ++i) {
+        for (size_t st = 0; st < n; ++st)
+          for (size_t b = 0; b < kData * S; b += 8) {
+            const uint64_t v = r();
+            std::memcpy(h + st * stripe + b, &v, 8);
+          }
+        if (xrs_encode_host(x->codec(), h, S, S, stripe, n)) ++bad;
+        std::vector<uint8_t> orig(h, h + n * stripe);
+        const int a = static_cast<int>(r() % kData), b = (a + 1 + static_cast<int>(r() % (kData - 1))) % kData;
+        const int lost[2] = {a, b};
+        std::vector<int> has;
+        for (int j = 0; j < kData + kParity; ++j)
+          if (j != a && j != b) has.push_back(j);
+        for (size_t st = 0; st < n; ++st)
+          for (int j : lost) std::memset(h + st * stripe + j * S, 0x5a, S);
+        if (xrs_reconst_host(x->codec(), h, S, S, stripe, n, has.data(), static_cast<int>(has.size()), lost, 2))
+          ++bad;
+        for (size_t st = 0; st < n; ++st)
+          if (std::memcmp(h + st * stripe, orig.data() + st * stripe, kData * S) != 0) ++bad;
+      }
+      xrs_host_free(h);
+    });
+  for (auto& t : th) t.join();
+  xrs_trace_kernels(0);
+  std::string names(xrs_traced_kernels(nullptr, 0) + 1, '\0');
+  xrs_traced_kernels(&names[0], names.size());
+  unsetenv("XRS_WSP");
+  unsetenv("XRS_WSP_GRID");
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+  if (names.find("staged_wsp_kernel<12, ") == std::string::npos)
+    FATAL("the persistent kernel did not run: %s", names.c_str());
+}
+
 // A vect shorter or longer than vects[0] is rejected before the C ABI call
 // (which reads and writes `size` bytes of every vect): ADVICE r1.
 static void TestMismatchedVects() {
@@ -450,6 +508,7 @@ int main(int argc, char** argv) {
       {"TestQueue_Concurrent", TestQueue_Concurrent, true},
       {"TestQueue_Oversubscribed", TestQueue_Oversubscribed, true},
       {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
+      {"TestXRS_ReconstPersistent", TestXRS_ReconstPersistent, true},
   };
   for (const T& t : tests) {
     if (cpu_only && t.gpu) continue;

@@ -444,7 +444,7 @@ def headline(R: Rank, args):
     # algorithmic bytes per launch, read bytes per launch, launcher).  The
     # line reports the kernel the library actually launched (traced below).
     launches = [
-        ("encode_4k", "pair_kernel<4, 12, false, true, 128, false>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
+        ("encode_4k", "enc_ws_kernel<12, 256>", n_enc * (D + P) * ENC_S, n_enc * D * ENC_S,
          lambda i: x.encode_batched(enc_buf.data_ptr(), ENC_S, enc_shard, enc_stripe, n_enc, s)),
         ("reconst_one_4k", "rows_kernel<2, 12, 4, false, true, 256>", n_enc * 9 * ENC_S,
          n_enc * 8 * ENC_S,

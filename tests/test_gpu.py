@@ -251,9 +251,16 @@ def oracle_encode_batch(o, host):
 
 
 # 1 MiB and 1 MiB + 2: the 12+4 Encode from 512 KiB halves runs the
-# plain-order kernel specialization (pair_kernel<4, 12, false, true, 128, true>)
-@pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 65536, 1 << 20, (1 << 20) + 2])
-def test_encode_batched_vs_oracle(cuda, rng, size):
+# plain-order kernel specialization (pair_kernel<4, 12, false, true, 128, true>);
+# aligned halves up to 128 KiB the wave-specialised enc_ws_kernel<12, 256>
+# (XRS_ENC_WS=0: the pair kernel there too; =128 / 512: other block sizes).
+@pytest.mark.parametrize("enc_ws", ["", "0", "128", "512"])
+@pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 4128, 65536, 262144, 1 << 20, (1 << 20) + 2])
+def test_encode_batched_vs_oracle(cuda, rng, monkeypatch, size, enc_ws):
+    if enc_ws:
+        monkeypatch.setenv("XRS_ENC_WS", enc_ws)
+    else:
+        monkeypatch.delenv("XRS_ENC_WS", raising=False)
     n = max(3, (8 << 20) // (16 * size))
     host = batch(rng, n, size)
     t = to_dev(host, cuda)

@@ -39,7 +39,7 @@ def codec():
 
 
 @pytest.mark.parametrize("size,n,enc,rec", [
-    (4096, 1024, "pair_kernel<4, 12, false, true, 128, false>",
+    (4096, 1024, "enc_ws_kernel<12, 256>",
      "rows_kernel<2, 12, 4, false, true, 256>"),
     (1 << 20, 8, "pair_kernel<4, 12, false, true, 128, true>",
      "rows_kernel<2, 12, 4, false, true, 1024>"),

@@ -26,7 +26,7 @@ from collections import defaultdict
 
 # bench.py kernel keys -> (kernel-name fragment, grid threads of the timed launch)
 KERNELS = {
-    "encode_4k": ("pair_kernel<4, 12, false, true, 128, false>", 65536 * 128),
+    "encode_4k": ("enc_ws_kernel<12, 256>", 65536 * 256),
     "reconst_one_4k": ("rows_kernel<2, 12, 4, false, true, 256>", 65536 * 128),
     "encode_1m": ("pair_kernel<4, 12, false, true, 128, true>", 512 * 32768),
     "reconst_one_1m": ("rows_kernel<2, 12, 4, false, true, 1024>", 512 * 32768),

@@ -851,6 +851,69 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
   for (int u = 0; u < NN; ++u) stw<W>(ob[u], row_addr(a.bdst[u], stripe, off));
 }
 
+// Wave-specialised 12+4-style Encode (compile-time source count C, P = 4,
+// 16-byte chunks, halves a multiple of 16 bytes): a block of 2*T lanes works
+// on T chunks.  Lanes [0, T) load the C data a-halves, form the four parity
+// a-halves and store them, and leave the piggyback terms (data c rides on
+// parity 1 + c % 3, xrs.go:77-100) in LDS; lanes [T, 2T) load the C data
+// b-halves and form the four RS b-halves at the same time; one barrier; the
+// b-lanes add the piggyback terms and store.  Each lane holds one half's rows
+// (the pair kernel holds both, 170 VGPRs, two waves per SIMD).
+template <int C, int T>
+__global__ __launch_bounds__(2 * T) void enc_ws_kernel(const PairArgs<4, C, true> a) {
+  constexpr int P = 4, W = 4;
+  __shared__ uint4 xfer[P - 1][T];
+  const bool blane = threadIdx.x >= T;
+  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
+  const uint64_t gid = logical_block(a.order) * T + t;
+  const bool valid = gid < a.total;
+  const uint64_t stripe = gid / a.chunks;
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W) + (blane ? a.half : 0);
+  uint32_t acc[P][W];
+  if (valid) {
+    uint32_t x[C][W];
+#pragma unroll
+    for (int c = 0; c < C; ++c) ldw<W>(x[c], row_addr(a.src[c], stripe, off));
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+#pragma unroll
+    for (int c = 0; c + 1 < C; c += 2) rows_mac2<P, W>(acc, a.tab[c], a.tab[c + 1], x[c], x[c + 1]);
+    if constexpr (C & 1) rows_mac1<P, W>(acc, a.tab[C - 1], x[C - 1]);
+    if (!blane) {
+      uint32_t pg[P - 1][W];
+#pragma unroll
+      for (int r = 0; r < P - 1; ++r)
+#pragma unroll
+        for (int w = 0; w < W; ++w) pg[r][w] = 0u;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int w = 0; w < W; ++w) pg[c % (P - 1)][w] ^= x[c][w];
+#pragma unroll
+      for (int r = 0; r < P - 1; ++r) xfer[r][t] = make_uint4(pg[r][0], pg[r][1], pg[r][2], pg[r][3]);
+#pragma unroll
+      for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(a.dst[r], stripe, off));
+    }
+  }
+  // LDS only: no wait on the a-lanes' stores at the barrier.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  if (!blane || !valid) return;
+#pragma unroll
+  for (int r = 1; r < P; ++r) {
+    const uint4 v = xfer[r - 1][t];
+    acc[r][0] ^= v.x;
+    acc[r][1] ^= v.y;
+    acc[r][2] ^= v.z;
+    acc[r][3] ^= v.w;
+  }
+#pragma unroll
+  for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(a.dst[r], stripe, off));
+}
+
 // Persistent form of staged_ws_kernel for 2 lost data vects from 256 to 768
 // KiB halves: one block of 2*T lanes per CU takes T-chunk tiles from a launch-wide
 // counter, as the hardware dispatcher hands out blocks (so the tiles in
@@ -1845,6 +1908,28 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   if (ACC && VEC && p.half <= 4096 && !forced) a.order.k = static_cast<uint32_t>(blocks / 8);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   if constexpr (VEC && P == 4 && C == 12 && !ACC) {
+    // The wave-specialised Encode (enc_ws_kernel), 256 chunks per block of
+    // 512 lanes, on halves a multiple of 16 bytes up to 128 KiB (bytes moved,
+    // interleaved medians vs the pair kernel, profiles/r04_encws_mid.log:
+    // 4 / 8 / 32 / 64 / 128 / 256 KiB vects +3.6 / +3.8 / +4.2 / +4.7 /
+    // -0.5 / +3.7%; 384 KiB -1%, 512 KiB -3%, 1 MiB -1.6..+1.1%, so larger
+    // halves keep the pair kernel; r04_encws_4k.log, r04_encws_order.log).
+    // XRS_ENC_WS=0 turns it off, =128 / 256 / 512 forces a block size (A/B).
+    const char* ew = std::getenv("XRS_ENC_WS");
+    const bool ws_on = (ew && *ew) ? ew[0] != '0' : p.half <= (128u << 10);
+    if (ws_on && p.half % 16 == 0) {
+      const int T = (ew && *ew) ? std::atoi(ew) : 256;
+      const uint64_t tb = (a.total + T - 1) / T;
+      if (tb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+      a.order = block_order(Shape::kPair, VEC, p.half, tb, T);
+      if (const char* e = std::getenv("XRS_ENC_WS_ORDER"))  // A/B
+        a.order.k = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+      const dim3 g(static_cast<unsigned>(tb));
+      if (T == 128) XRS_LAUNCH((enc_ws_kernel<12, 128>), g, dim3(256), stream, a);
+      else if (T == 512) XRS_LAUNCH((enc_ws_kernel<12, 512>), g, dim3(1024), stream, a);
+      else XRS_LAUNCH((enc_ws_kernel<12, 256>), g, dim3(512), stream, a);
+      return static_cast<int>(hipGetLastError());
+    }
     if (plain12) {
       XRS_LAUNCH((pair_kernel<P, C, ACC, VEC, 128, true>), dim3(static_cast<unsigned>(blocks)),
                          dim3(128), stream, a);

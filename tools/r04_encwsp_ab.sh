@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 4: the persistent counter-fed Encode (XRS_ENC_WSP=T) against the
+# Round 4: the persistent counter-fed Encode (XRS_ENC_WSP=T; the kernel,
+# enc_wsp_kernel, is in commit 416ee77 only: slower at every size, removed) against the
 # default launch: oracle tests forced (also with 24-block grids, so blocks
 # take many tiles), then an interleaved A/B, bytes moved.
 set -u

@@ -1105,141 +1105,6 @@ __global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, 
   }
 }
 
-// Persistent, counter-fed form of enc_ws_kernel (the staged_wsp_kernel
-// scheme applied to Encode; A/B: XRS_ENC_WSP): one block of 2*T lanes per CU
-// takes T-chunk tiles from a launch-wide counter; per tile the a-lanes load,
-// form and store the parity a-halves and leave the piggyback terms in LDS slot
-// j & 1, the b-lanes form the RS b-halves from rows issued one tile earlier;
-// one barrier; the b-lanes add the terms, store and issue the next tile's
-// rows while the a-lanes already load theirs.
-template <int C, int T>
-__global__ __launch_bounds__(2 * T) void enc_wsp_kernel(const PairArgs<4, C, true> a,
-                                                         const uint32_t ntiles, uint32_t* ctr) {
-  using Args = PairArgs<4, C, true>;
-  constexpr int P = 4, W = 4;
-  __shared__ uint4 xfer[2][P - 1][T];
-  __shared__ uint32_t nexttile[2];
-  const bool blane = __builtin_amdgcn_readfirstlane(threadIdx.x) >= T;
-  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
-  uint32_t v = blockIdx.x;
-  uint32_t x[C][W];
-  if (!blane) {
-    for (uint32_t j = 0; v < ntiles; ++j) {
-      const XRS_KC Args* q = kargs<Args>();
-      const uint32_t s = j & 1u;
-      uint32_t nv = 0;
-      if (threadIdx.x == 0) nv = atomicAdd(ctr, 1u) + gridDim.x;
-      const uint64_t gid = logical_of(kld(q->order), v) * T + t;
-      if (gid < q->total) {
-        const uint64_t chunks = q->chunks;
-        const uint64_t stripe = gid / chunks;
-        const uint64_t off = q->off0 + (gid - stripe * chunks) * (4 * W);
-#pragma unroll
-        for (int c = 0; c < C; ++c) ldw<W>(x[c], row_addr(kld(q->src[c]), stripe, off));
-        uint32_t acc[P][W];
-#pragma unroll
-        for (int r = 0; r < P; ++r)
-#pragma unroll
-          for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-#pragma unroll
-        for (int c = 0; c + 1 < C; c += 2) {
-          GfTab t0[P], t1[P];
-          ktabs<P>(t0, q->tab[c]);
-          ktabs<P>(t1, q->tab[c + 1]);
-          rows_mac2<P, W>(acc, t0, t1, x[c], x[c + 1]);
-        }
-        if constexpr (C & 1) {
-          GfTab t0[P];
-          ktabs<P>(t0, q->tab[C - 1]);
-          rows_mac1<P, W>(acc, t0, x[C - 1]);
-        }
-        uint32_t pg[P - 1][W];
-#pragma unroll
-        for (int r = 0; r < P - 1; ++r)
-#pragma unroll
-          for (int w = 0; w < W; ++w) pg[r][w] = 0u;
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int w = 0; w < W; ++w) pg[c % (P - 1)][w] ^= x[c][w];
-#pragma unroll
-        for (int r = 0; r < P - 1; ++r) xfer[s][r][t] = make_uint4(pg[r][0], pg[r][1], pg[r][2], pg[r][3]);
-#pragma unroll
-        for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(kld(q->dst[r]), stripe, off));
-      }
-      if (threadIdx.x == 0) nexttile[s ^ 1u] = nv;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      v = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
-    }
-    return;
-  }
-  if (v < ntiles) {
-    const uint64_t gid = logical_of(a.order, v) * T + t;
-    if (gid < a.total) {
-      const uint64_t stripe = gid / a.chunks;
-      const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W) + a.half;
-#pragma unroll
-      for (int c = 0; c < C; ++c) ldw<W>(x[c], row_addr(a.src[c], stripe, off));
-    }
-  }
-  for (uint32_t j = 0; v < ntiles; ++j) {
-    const XRS_KC Args* q = kargs<Args>();
-    const uint32_t s = j & 1u;
-    const BlockOrder order = kld(q->order);
-    const uint64_t total = q->total, chunks = q->chunks, off0 = q->off0, half = q->half;
-    const uint64_t gid = logical_of(order, v) * T + t;
-    uint32_t acc[P][W];
-#pragma unroll
-    for (int r = 0; r < P; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-    if (gid < total) {
-#pragma unroll
-      for (int c = 0; c + 1 < C; c += 2) {
-        GfTab t0[P], t1[P];
-        ktabs<P>(t0, q->tab[c]);
-        ktabs<P>(t1, q->tab[c + 1]);
-        rows_mac2<P, W>(acc, t0, t1, x[c], x[c + 1]);
-      }
-      if constexpr (C & 1) {
-        GfTab t0[P];
-        ktabs<P>(t0, q->tab[C - 1]);
-        rows_mac1<P, W>(acc, t0, x[C - 1]);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    if (gid < total) {
-      const uint64_t stripe = gid / chunks;
-      const uint64_t off = off0 + (gid - stripe * chunks) * (4 * W) + half;
-#pragma unroll
-      for (int r = 1; r < P; ++r) {
-        const uint4 e = xfer[s][r - 1][t];
-        acc[r][0] ^= e.x;
-        acc[r][1] ^= e.y;
-        acc[r][2] ^= e.z;
-        acc[r][3] ^= e.w;
-      }
-#pragma unroll
-      for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(kld(q->dst[r]), stripe, off));
-    }
-    const uint32_t vn = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
-    if (vn < ntiles) {
-      const uint64_t gn = logical_of(order, vn) * T + t;
-      if (gn < total) {
-        const uint64_t sn = gn / chunks;
-        const uint64_t on = off0 + (gn - sn * chunks) * (4 * W) + half;
-#pragma unroll
-        for (int c = 0; c < C; ++c) ldw<W>(x[c], row_addr(kld(q->src[c]), sn, on));
-      }
-    }
-    v = vn;
-  }
-}
-
 // Runtime-count form of staged_ws_kernel (any codec with d <= 16, lost parity
 // in the pattern, nl != nn): a-lanes load na a-rows, b-lanes nb b-rows, each
 // role's guarded loads issued together (each role waits once, so the
@@ -2050,39 +1915,6 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
     // -0.5 / +3.7%; 384 KiB -1%, 512 KiB -3%, 1 MiB -1.6..+1.1%, so larger
     // halves keep the pair kernel; r04_encws_4k.log, r04_encws_order.log).
     // XRS_ENC_WS=0 turns it off, =128 / 256 / 512 forces a block size (A/B).
-    if (const char* pw = std::getenv("XRS_ENC_WSP"); pw && *pw && pw[0] != '0' && p.half % 16 == 0) {
-      // A/B: the persistent counter-fed form, T = XRS_ENC_WSP, K = the tiles
-      // of one half-vect (XRS_ENC_WS_ORDER overrides).
-      const int T = std::atoi(pw) == 256 ? 256 : 512;
-      const uint64_t tiles = (a.total + T - 1) / T;
-      if (tiles > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
-      a.order = block_order(Shape::kPair, VEC, p.half, tiles, T);
-      a.order.k = static_cast<uint32_t>(std::max<uint64_t>(1, a.chunks / T));
-      if (const char* e = std::getenv("XRS_ENC_WS_ORDER")) a.order.k = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
-      uint64_t per_cu = 1;
-      if (const char* e = std::getenv("XRS_WSP_PER_CU")) per_cu = std::max<uint64_t>(1, std::strtoul(e, nullptr, 10));
-      uint64_t grid = per_cu * static_cast<uint64_t>(cu_count(stream));
-      if (const char* e = std::getenv("XRS_WSP_GRID")) grid = std::max<uint64_t>(1, std::strtoul(e, nullptr, 10));
-      grid = std::min<uint64_t>(tiles, grid);
-      uint32_t* ctr = nullptr;
-      const hipMemPool_t pool = counter_pool(stream);
-      const hipError_t ae =
-          pool ? hipMallocFromPoolAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), pool, stream)
-               : hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), stream);
-      if (ae == hipSuccess) {
-        hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), stream);
-        if (e == hipSuccess) {
-          const dim3 g(static_cast<unsigned>(grid));
-          const uint32_t nt = static_cast<uint32_t>(tiles);
-          if (T == 256) XRS_LAUNCH((enc_wsp_kernel<12, 256>), g, dim3(512), stream, a, nt, ctr);
-          else XRS_LAUNCH((enc_wsp_kernel<12, 512>), g, dim3(1024), stream, a, nt, ctr);
-          e = hipGetLastError();
-        }
-        const hipError_t f = hipFreeAsync(ctr, stream);
-        return static_cast<int>(e != hipSuccess ? e : f);
-      }
-      (void)hipGetLastError();
-    }
     const char* ew = std::getenv("XRS_ENC_WS");
     const bool ws_on = (ew && *ew) ? ew[0] != '0' : p.half <= (128u << 10);
     if (ws_on && p.half % 16 == 0) {

@@ -583,16 +583,21 @@ CT_CODECS = [(4, 2), (6, 3), (8, 4), (10, 4), (12, 3), (14, 4), (16, 4), (20, 4)
              (8, 3), (10, 3), (12, 2)]
 
 
-@pytest.mark.parametrize("mode", ["ct", "dyn"])
+@pytest.mark.parametrize("mode", ["ct", "dyn", "ws"])
 @pytest.mark.parametrize("d,p", CT_CODECS)
 def test_compile_time_shapes_batched_vs_oracle(cuda, rng, monkeypatch, mode, d, p):
-    """The compile-time Encode (pair_kernel<p, d>) and ReconstOne
-    (rows_kernel<2, d, |XORSet(bi)|>) shapes of common codecs, and the
-    runtime-count kernels they replace (XRS_ENCODE_DYN / XRS_ROWS_DYN), on
-    batches against the oracle: every k, aligned and ragged sizes."""
+    """The compile-time Encode (pair_kernel<p, d>; enc_ws_kernel<d, 256> for
+    d+4 when XRS_ENC_WS forces it) and ReconstOne (rows_kernel<2, d,
+    |XORSet(bi)|>) shapes of common codecs, and the runtime-count kernels they
+    replace (XRS_ENCODE_DYN / XRS_ROWS_DYN), on batches against the oracle:
+    every k, aligned and ragged sizes."""
     if mode == "dyn":
         monkeypatch.setenv("XRS_ENCODE_DYN", "1")
         monkeypatch.setenv("XRS_ROWS_DYN", "1")
+    if mode == "ws":
+        if p != 4:
+            pytest.skip("the wave-specialised Encode is a d+4 shape")
+        monkeypatch.setenv("XRS_ENC_WS", "256")
     x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
     for size, n in ((4096, 64), (4100, 33), (34, 50)):
         host = rng.integers(0, 256, size=(n, d + p, size), dtype=np.uint8)

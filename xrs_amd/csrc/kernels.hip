@@ -1907,29 +1907,39 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
   if (enc12 && huge) a.order.k = 128;
   if (ACC && VEC && p.half <= 4096 && !forced) a.order.k = static_cast<uint32_t>(blocks / 8);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
-  if constexpr (VEC && P == 4 && C == 12 && !ACC) {
+  if constexpr (VEC && P == 4 && C != kDyn && !ACC) {
     // The wave-specialised Encode (enc_ws_kernel), 256 chunks per block of
     // 512 lanes, on halves a multiple of 16 bytes up to 128 KiB (bytes moved,
     // interleaved medians vs the pair kernel, profiles/r04_encws_mid.log:
     // 4 / 8 / 32 / 64 / 128 / 256 KiB vects +3.6 / +3.8 / +4.2 / +4.7 /
     // -0.5 / +3.7%; 384 KiB -1%, 512 KiB -3%, 1 MiB -1.6..+1.1%, so larger
     // halves keep the pair kernel; r04_encws_4k.log, r04_encws_order.log).
-    // XRS_ENC_WS=0 turns it off, =128 / 256 / 512 forces a block size (A/B).
+    // The same holds for 8+4 and 10+4 (4 / 64 KiB vects +4.5 / +0.9% and
+    // +8.8 / +1.9%), not for 14+4, 16+4 (-1.9..+1.5%) or 20+4 (-13..-19%,
+    // 134 VGPRs): profiles/r04_encws_codecs.log.  XRS_ENC_WS forces it for
+    // every d+4 compile-time shape (A/B); =0 turns it off, =128 / 256 / 512
+    // sets the block size (12+4; 256 for the others).
     const char* ew = std::getenv("XRS_ENC_WS");
-    const bool ws_on = (ew && *ew) ? ew[0] != '0' : p.half <= (128u << 10);
+    const bool ws_on = (ew && *ew) ? ew[0] != '0' : (C <= 12 && p.half <= (128u << 10));
     if (ws_on && p.half % 16 == 0) {
-      const int T = (ew && *ew) ? std::atoi(ew) : 256;
+      const int T = (C == 12 && ew && *ew) ? std::atoi(ew) : 256;
       const uint64_t tb = (a.total + T - 1) / T;
       if (tb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
       a.order = block_order(Shape::kPair, VEC, p.half, tb, T);
       if (const char* e = std::getenv("XRS_ENC_WS_ORDER"))  // A/B
         a.order.k = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
       const dim3 g(static_cast<unsigned>(tb));
-      if (T == 128) XRS_LAUNCH((enc_ws_kernel<12, 128>), g, dim3(256), stream, a);
-      else if (T == 512) XRS_LAUNCH((enc_ws_kernel<12, 512>), g, dim3(1024), stream, a);
-      else XRS_LAUNCH((enc_ws_kernel<12, 256>), g, dim3(512), stream, a);
+      if constexpr (C == 12) {
+        if (T == 128) XRS_LAUNCH((enc_ws_kernel<12, 128>), g, dim3(256), stream, a);
+        else if (T == 512) XRS_LAUNCH((enc_ws_kernel<12, 512>), g, dim3(1024), stream, a);
+        else XRS_LAUNCH((enc_ws_kernel<12, 256>), g, dim3(512), stream, a);
+      } else {
+        XRS_LAUNCH((enc_ws_kernel<C, 256>), g, dim3(512), stream, a);
+      }
       return static_cast<int>(hipGetLastError());
     }
+  }
+  if constexpr (VEC && P == 4 && C == 12 && !ACC) {
     if (plain12) {
       XRS_LAUNCH((pair_kernel<P, C, ACC, VEC, 128, true>), dim3(static_cast<unsigned>(blocks)),
                          dim3(128), stream, a);

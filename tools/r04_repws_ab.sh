@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 4: the wave-specialised Replace (XRS_REP_WS=1) against the
+# Round 4: the wave-specialised Replace (XRS_REP_WS=1; rep_ws_kernel is in
+# commit b73a498 only: within +-3%, removed) against the
 # accumulating pair kernel: oracle tests forced, then an interleaved A/B
 # (bytes moved), Replace(1 / 4 / 8) at 4 KiB, 64 KiB and 8 MiB vects.
 set -u

@@ -914,64 +914,6 @@ __global__ __launch_bounds__(2 * T) void enc_ws_kernel(const PairArgs<4, C, true
   for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(a.dst[r], stripe, off));
 }
 
-// Wave-specialised Replace (accumulating pair kernel, P = 4 parity rows, C
-// replaced data rows; A/B: XRS_REP_WS): lanes [0, T) read the C data
-// a-halves and the four parity a-halves, add the GF terms, store, and leave
-// each output's piggyback term (the data a-halves in its pbmask) in LDS;
-// lanes [T, 2T) do the same for the b-halves; one barrier; the b-lanes add
-// the terms and store (xrs.go:363-387).
-template <int C, int T>
-__global__ __launch_bounds__(2 * T) void rep_ws_kernel(const PairArgs<4, C, true> a) {
-  constexpr int P = 4, W = 4;
-  __shared__ uint4 xfer[P][T];
-  const bool blane = threadIdx.x >= T;
-  const uint32_t t = blane ? threadIdx.x - T : threadIdx.x;
-  const uint64_t gid = logical_block(a.order) * T + t;
-  const bool valid = gid < a.total;
-  const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W) + (blane ? a.half : 0);
-  uint32_t acc[P][W];
-  if (valid) {
-    uint32_t x[C][W];
-#pragma unroll
-    for (int r = 0; r < P; ++r) ldw<W>(acc[r], row_addr(a.dst[r], stripe, off));
-#pragma unroll
-    for (int c = 0; c < C; ++c) ldw<W>(x[c], row_addr(a.src[c], stripe, off));
-#pragma unroll
-    for (int c = 0; c + 1 < C; c += 2) rows_mac2<P, W>(acc, a.tab[c], a.tab[c + 1], x[c], x[c + 1]);
-    if constexpr (C & 1) rows_mac1<P, W>(acc, a.tab[C - 1], x[C - 1]);
-    if (!blane) {
-#pragma unroll
-      for (int r = 0; r < P; ++r) {
-        uint32_t pg[W] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const uint32_t m = 0u - ((a.pbmask[r] >> c) & 1u);
-#pragma unroll
-          for (int w = 0; w < W; ++w) pg[w] = xor_masked(pg[w], x[c][w], m);
-        }
-        xfer[r][t] = make_uint4(pg[0], pg[1], pg[2], pg[3]);
-      }
-#pragma unroll
-      for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(a.dst[r], stripe, off));
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  if (!blane || !valid) return;
-#pragma unroll
-  for (int r = 0; r < P; ++r) {
-    const uint4 v = xfer[r][t];
-    acc[r][0] ^= v.x;
-    acc[r][1] ^= v.y;
-    acc[r][2] ^= v.z;
-    acc[r][3] ^= v.w;
-  }
-#pragma unroll
-  for (int r = 0; r < P; ++r) stw<W>(acc[r], row_addr(a.dst[r], stripe, off));
-}
-
 // Persistent form of staged_ws_kernel for 2 lost data vects from 256 to 768
 // KiB halves: one block of 2*T lanes per CU takes T-chunk tiles from a launch-wide
 // counter, as the hardware dispatcher hands out blocks (so the tiles in
@@ -1994,22 +1936,6 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
       } else {
         XRS_LAUNCH((enc_ws_kernel<C, 256>), g, dim3(512), stream, a);
       }
-      return static_cast<int>(hipGetLastError());
-    }
-  }
-  if constexpr (VEC && P == 4 && C != kDyn && ACC) {
-    // A/B: the wave-specialised Replace (XRS_REP_WS=1; halves a multiple of
-    // 16 bytes), 256 chunks per block of 512 lanes.
-    const char* rw = std::getenv("XRS_REP_WS");
-    if (rw && rw[0] == '1' && p.half % 16 == 0) {
-      constexpr int T = 256;
-      const uint64_t tb = (a.total + T - 1) / T;
-      if (tb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
-      a.order = block_order(Shape::kPair, VEC, p.half, tb, T);
-      if (p.half <= 4096) a.order.k = static_cast<uint32_t>(tb / 8);
-      if (const char* e = std::getenv("XRS_ENC_WS_ORDER"))  // A/B
-        a.order.k = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
-      XRS_LAUNCH((rep_ws_kernel<C, T>), dim3(static_cast<unsigned>(tb)), dim3(2 * T), stream, a);
       return static_cast<int>(hipGetLastError());
     }
   }

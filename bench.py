@@ -782,7 +782,7 @@ def per_stripe_queue(args):
     if not os.path.exists(exe):
         return {"skipped": "tools/sync_bench not built (build() makes it)"}
     def child(mode):
-        cmd = [exe, "4096", mode] + (["50"] if mode == "queue" else []) + [
+        cmd = [exe, "4096", mode] + (["50"] if mode.startswith("queue") else []) + [
             str(t) for t in args.queue_callers]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
@@ -801,13 +801,22 @@ def per_stripe_queue(args):
                       for x in lines},
                   "cpu_note": ("cpu_cores = process CPU time (callers' copies + the queue's "
                                "launcher and completion threads) / wall time")}
+    # the same callers with their vects in registered memory (xrs_host_alloc:
+    # the cgo shim's pinned buffer pool): no CPU copy through staging, the
+    # queue's gather / scatter kernels move the rows (queue.cpp table mode)
+    lines, err = child("queuereg")
+    out["registered"] = err or {"by_callers": {str(x["threads"]): {k: x[k] for k in (
+        "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch", "wait_us_per_batch",
+        "cpu_cores", "cpu_seconds_per_gib") if k in x} for x in lines}}
     # the plain drop-in call (xrs_encode per stripe) from the same number of
     # threads on ONE codec: contended calls batch through the codec's queue
-    lines, err = child("syncmt")
-    out["plain_api"] = err or {
-        x["api"].split()[0]: {str(x["threads"]): {k: x[k] for k in (
+    def plain(mode):
+        lines, err = child(mode)
+        return err or {x["api"].split()[0]: {str(x["threads"]): {k: x[k] for k in (
             "gibps", "calls_per_s", "cpu_cores", "cpu_seconds_per_gib") if k in x}}
-        for x in lines}
+            for x in lines}
+    out["plain_api"] = plain("syncmt")
+    out["plain_api_registered"] = plain("syncmtreg")
     return out
 
 

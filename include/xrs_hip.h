@@ -292,6 +292,10 @@ size_t xrs_queue_batch_stripes(const xrs_queue *q);
  * out[2] ns from each batch's launch to its completion, out[3] ns each batch
  * waited between opening and launch (summed over batches). */
 int xrs_queue_stats(xrs_queue *q, uint64_t out[4]);
+/* Batches run since xrs_queue_new by stripe count: counts[n] = batches of n
+ * stripes for n < cap - 1, counts[cap - 1] = batches of cap - 1 or more
+ * (stripe counts past 64 are kept as 64). */
+int xrs_queue_batch_sizes(xrs_queue *q, uint64_t *counts, int cap);
 /* Diagnostics: the queue's state (per staging batch: state, slots reserved /
  * staged / released, launches and the completion word) as text into buf
  * (NUL-terminated, truncated to cap); returns the full length.  Takes the

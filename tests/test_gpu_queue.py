@@ -488,3 +488,57 @@ def test_shared_codec_concurrent_sync_calls(size):
         t.join(timeout=120)
     assert not any(t.is_alive() for t in th), "a caller hung"
     assert not errors, errors[:3]
+
+
+def test_queue_coalesces_barrier_released_callers():
+    """32 threads released together by a barrier, each making one 4 KiB
+    Encode and then one ReconstOne call per round on ONE queue (the
+    reference's per-stripe call pattern, xrs_test.go:498-521): the queue
+    must run them in fewer batches than calls, several of them holding 4
+    stripes or more (xrs_queue_batch_sizes), and every call is bit-exact to
+    the oracle."""
+    size, n_threads, rounds = 4096, 32, 6
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size)
+    rng = np.random.Generator(np.random.PCG64(9100))
+    work = []
+    for t in range(n_threads):
+        per = []
+        for r in range(rounds):
+            v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+            ref = [a.copy() for a in v]
+            o.encode(ref)
+            per.append((v, ref, int(rng.integers(0, D))))
+        work.append(per)
+    bar = threading.Barrier(n_threads)
+    errors = []
+
+    def worker(t):
+        try:
+            for r, (v, ref, k) in enumerate(work[t]):
+                bar.wait(timeout=60)
+                q.encode(v)
+                assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, r)
+                v[k][:] = 0x3C
+                bar.wait(timeout=60)
+                q.reconst_one(v, k)
+                assert np.array_equal(v[k], ref[k]), ("rec", t, r, k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a caller hung:\n" + q.dump()
+    st, sizes = q.stats(), q.batch_sizes()
+    q.close()
+    assert not errors, errors[:3]
+    calls = n_threads * rounds * 2
+    print(f"queue: {calls} calls in {st['batches']} batches, stripes per batch {sizes}")
+    assert st["stripes"] == calls, st
+    assert sum(n * c for n, c in sizes.items()) == calls, sizes
+    assert st["batches"] < calls // 2, (st, sizes)
+    assert sum(c for n, c in sizes.items() if n >= 4) >= 3, sizes

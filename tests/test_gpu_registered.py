@@ -1,0 +1,309 @@
+"""GPU tests of the per-stripe calls on caller-registered host memory: vects
+inside ranges pinned and mapped by xrs_host_alloc / xrs_host_register run
+without the CPU gather / scatter through pinned staging -- in place over PCIe
+for a lone sync call (codec.cpp reg_vects), and through the queue's gather /
+scatter kernels for coalesced calls (queue.cpp table mode, copy_kernel).
+Every result, side effects included, is compared with the oracle
+(oracle/xrs_oracle.c, following xrs.go:103-387)."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+pytestmark = pytest.mark.gpu
+D, P = 12, 4
+PAGE = 4096
+
+
+class Arena:
+    """Host memory the library knows as pinned and mapped: `alloc` from
+    xrs_host_alloc, `register` a numpy buffer passed to xrs_host_register.
+    take(n, skew) hands out n-byte vects, each starting `skew` bytes past a
+    16-byte boundary (Go slices and numpy views need not be aligned)."""
+
+    def __init__(self, nbytes, kind):
+        self.kind = kind
+        L = xrs_amd.lib()
+        if kind == "alloc":
+            self.ptr = L.xrs_host_alloc(nbytes)
+            assert self.ptr
+            self.buf = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+        else:
+            raw = np.empty(nbytes + PAGE, np.uint8)
+            off = (-raw.ctypes.data) % PAGE
+            self.raw = raw
+            self.buf = raw[off:off + nbytes]
+            self.ptr = self.buf.ctypes.data
+            assert L.xrs_host_register(self.ptr, nbytes) == 0
+        self.pos = 0
+
+    def take(self, n, skew=0):
+        start = (self.pos + 15) // 16 * 16 + skew
+        assert start + n <= len(self.buf), "arena too small"
+        self.pos = start + n
+        return self.buf[start:start + n]
+
+    def close(self):
+        L = xrs_amd.lib()
+        if self.kind == "alloc":
+            L.xrs_host_free(self.ptr)
+        else:
+            assert L.xrs_host_unregister(self.ptr) == 0
+
+
+def _fill(rng, arrs):
+    for a in arrs:
+        a[:] = rng.integers(0, 256, size=len(a), dtype=np.uint8)
+
+
+def _same(a, b):
+    return all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("size", [4096, 4098, 1 << 20])
+@pytest.mark.parametrize("kind,skew", [("alloc", 0), ("register", 3)])
+def test_sync_calls_in_place(size, kind, skew):
+    """All five per-stripe calls on registered vects run in place (the trace
+    records host:sync_in_place once per call) and equal the oracle, the
+    reference's Reconst side effects on surviving parity included."""
+    rng = np.random.Generator(np.random.PCG64(size + skew))
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    ar = Arena(24 * (size + 32), kind)
+    try:
+        v = [ar.take(size, skew) for _ in range(D + P)]
+        extra = [ar.take(size, skew) for _ in range(3)]
+        _fill(rng, v + extra)
+        xrs_amd.trace_kernels(True)
+        # Encode (xrs.go:103)
+        ref = [a.copy() for a in v]
+        o.encode(ref)
+        x.encode(v)
+        assert _same(v, ref), "encode"
+        # ReconstOne (xrs.go:175): vects outside the need set hold garbage
+        k = 7
+        a_need, b_need = x.get_need_vects(k)
+        for j in range(D + P):
+            if j != k and j not in a_need:
+                v[j][: size // 2] = 0xC3
+        v[k][:] = 0
+        x.reconst_one(v, k)
+        assert np.array_equal(v[k], ref[k]), "reconst_one"
+        for j in range(D + P):
+            v[j][:] = ref[j]
+        # Reconst (xrs.go:236) of two data vects and one piggybacked parity
+        lost = [1, 10, D + 2]
+        has = [j for j in range(D + P) if j not in lost]
+        for j in lost:
+            v[j][:] = 0x5A
+        want = [a.copy() for a in v]
+        o.reconst(want, has, lost)
+        x.reconst(v, has, lost)
+        assert _same(v, want), "reconst"
+        for j in range(D + P):
+            v[j][:] = ref[j]
+        # Update (xrs.go:324) of row 4 with new bytes
+        new = extra[0]
+        par = [a.copy() for a in ref[D:]]
+        o.update(ref[4], new, 4, par)
+        x.update(v[4], new, 4, v[D:])
+        assert _same(v[D:], par), "update"
+        # Replace (xrs.go:363) of rows 2 and 9 (zero -> data direction)
+        rows = [2, 9]
+        par2 = [a.copy() for a in v[D:]]
+        o.replace([extra[1], extra[2]], rows, par2)
+        x.replace([extra[1], extra[2]], rows, v[D:])
+        assert _same(v[D:], par2), "replace"
+        xrs_amd.trace_kernels(False)
+        tr = xrs_amd.traced_kernels()
+        assert tr.get("host:sync_in_place") == 5, tr
+    finally:
+        xrs_amd.trace_kernels(False)
+        ar.close()
+
+
+def test_sync_partly_registered_falls_back():
+    """A call with one vect outside registered memory copies as before (same
+    result, no in-place trace event); ReconstOne needs only its need set and
+    vect k registered."""
+    size = 4096
+    rng = np.random.Generator(np.random.PCG64(11))
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    ar = Arena(20 * (size + 32), "alloc")
+    try:
+        v = [ar.take(size) for _ in range(D + P)]
+        _fill(rng, v)
+        plain = np.array(v[3])  # ordinary pageable memory
+        mixed = v[:3] + [plain] + v[4:]
+        ref = [a.copy() for a in mixed]
+        o.encode(ref)
+        xrs_amd.trace_kernels(True)
+        x.encode(mixed)
+        assert _same(mixed, ref)
+        assert "host:sync_in_place" not in xrs_amd.traced_kernels()
+        # ReconstOne(8) reads only its need set (xrs.go:146-171): b-halves of
+        # 0..11 but 8 and of 12 and 15 (bi), a-halves of 2, 5 and 11; vects 13
+        # and 14 are never read, so they may live anywhere
+        a_need, b_need = x.get_need_vects(8)
+        assert a_need == [2, 5, 11] and b_need == [12, 15], (a_need, b_need)
+        w = list(v)
+        for j in range(D + P):
+            w[j][:] = ref[j]
+        w[13] = np.array(ref[13])
+        w[14] = None
+        w[8][:] = 0
+        xrs_amd.trace_kernels(True)
+        x.reconst_one([a if a is not None else np.zeros(size, np.uint8) for a in w], 8)
+        assert np.array_equal(w[8], ref[8])
+        assert xrs_amd.traced_kernels().get("host:sync_in_place") == 1
+        # a pageable vect inside the need set: the call copies
+        w[0] = np.array(ref[0])
+        w[8][:] = 0
+        xrs_amd.trace_kernels(True)
+        x.reconst_one([a if a is not None else np.zeros(size, np.uint8) for a in w], 8)
+        assert np.array_equal(w[8], ref[8])
+        assert "host:sync_in_place" not in xrs_amd.traced_kernels()
+    finally:
+        xrs_amd.trace_kernels(False)
+        ar.close()
+
+
+@pytest.mark.parametrize("size", [4096, 4098, 65536])
+def test_queue_registered_and_plain_callers(size):
+    """24 threads on one queue, barrier-released per round, every op kind
+    (Encode, ReconstOne, Reconst of one pattern, Update, Replace of one rows
+    set); even threads use registered vects, odd ones plain numpy, so batches
+    mix both (the gather / scatter kernels serve the plain slots from pinned
+    staging).  Every call equals the oracle; copy_kernel ran."""
+    n_th, rounds = 24, 3
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=64)
+    ar = Arena(n_th * 20 * (size + 32), "alloc")
+    lost, need = [0, 5, D + 1], [0, 5, D + 1]
+    has = [j for j in range(D + P) if j not in lost]
+    rows = [3, 8]
+    work = []
+    for t in range(n_th):
+        rng = np.random.Generator(np.random.PCG64(500 + t))
+        if t % 2 == 0:
+            v = [ar.take(size, t % 5) for _ in range(D + P)]
+            ex = [ar.take(size, t % 5) for _ in range(3)]
+        else:
+            v = [np.empty(size, np.uint8) for _ in range(D + P)]
+            ex = [np.empty(size, np.uint8) for _ in range(3)]
+        work.append((rng, v, ex))
+    bar = threading.Barrier(n_th)
+    olock = threading.Lock()
+    errors = []
+
+    def worker(t):
+        rng, v, ex = work[t]
+        try:
+            for r in range(rounds):
+                _fill(rng, v + ex)
+                ref = [a.copy() for a in v]
+                with olock:
+                    o.encode(ref)
+                bar.wait(timeout=60)
+                q.encode(v)
+                assert _same(v, ref), ("enc", t, r)
+                k = (t + r) % D
+                v[k][:] = 0
+                bar.wait(timeout=60)
+                q.reconst_one(v, k)
+                assert np.array_equal(v[k], ref[k]), ("rec1", t, r)
+                for j in lost:
+                    v[j][:] = 0x11
+                want = [a.copy() for a in v]
+                with olock:
+                    o.reconst(want, has, need)
+                bar.wait(timeout=60)
+                q.reconst(v, has, need)
+                assert _same(v, want), ("rec", t, r)
+                for j in range(D + P):
+                    v[j][:] = ref[j]
+                par = [a.copy() for a in ref[D:]]
+                with olock:
+                    o.update(ref[t % D], ex[0], t % D, par)
+                bar.wait(timeout=60)
+                q.update(v[t % D], ex[0], t % D, v[D:])
+                assert _same(v[D:], par), ("upd", t, r)
+                par2 = [a.copy() for a in v[D:]]
+                with olock:
+                    o.replace([ex[1], ex[2]], rows, par2)
+                bar.wait(timeout=60)
+                q.replace([ex[1], ex[2]], rows, v[D:])
+                assert _same(v[D:], par2), ("rep", t, r)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
+
+    xrs_amd.trace_kernels(True)
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_th)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    xrs_amd.trace_kernels(False)
+    alive = any(t.is_alive() for t in th)
+    st = q.stats()
+    dump = q.dump() if alive else ""
+    q.close()
+    ar.close()
+    assert not alive, "a caller hung:\n" + dump
+    assert not errors, errors[:3]
+    assert st["stripes"] == n_th * rounds * 5, st
+    tr = xrs_amd.traced_kernels()
+    assert tr.get("copy_kernel", 0) > 0, tr
+
+
+def test_shared_codec_registered_concurrent():
+    """The plain per-stripe calls from 16 threads on ONE codec with
+    registered vects: the lone caller runs in place, contended calls go
+    through the codec's automatic queue in table mode; bit-exact."""
+    size = 4096
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    ar = Arena(16 * 18 * (size + 32), "register")
+    errors = []
+    olock = threading.Lock()
+    vs = [([ar.take(size, 8) for _ in range(D + P)], ar.take(size, 8)) for _ in range(16)]
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(900 + t))
+        v, new = vs[t]
+        try:
+            for i in range(12):
+                _fill(rng, v + [new])
+                ref = [a.copy() for a in v]
+                with olock:
+                    o.encode(ref)
+                x.encode(v)
+                assert _same(v, ref), ("enc", t, i)
+                k = (t + i) % D
+                v[k][:] = 0
+                x.reconst_one(v, k)
+                assert np.array_equal(v[k], ref[k]), ("rec", t, i)
+                par = [a.copy() for a in ref[D:]]
+                with olock:
+                    o.update(ref[k], new, k, par)
+                x.update(v[k], new, k, v[D:])
+                assert _same(v[D:], par), ("upd", t, i)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    xrs_amd.trace_kernels(True)
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    xrs_amd.trace_kernels(False)
+    alive = any(t.is_alive() for t in th)
+    ar.close()
+    assert not alive, "a caller hung"
+    assert not errors, errors[:3]
+    tr = xrs_amd.traced_kernels()
+    assert tr.get("host:sync_in_place", 0) + tr.get("copy_kernel", 0) > 0, tr

@@ -18,12 +18,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "xrs_amd", "libxrs_hip.so")
 LLVM = "/opt/rocm/llvm/bin"
 
-# (symbol regex, max VGPRs) -- the kernels bench.py and smoke() run
+# (symbol regex, max VGPRs) -- the kernels bench.py and smoke() run.  A bound
+# is the count up to which a compute unit still holds as many of the kernel's
+# blocks as it does now (512 VGPRs per SIMD lane, allocated in 8s): 128 keeps
+# four waves per SIMD, which is two 512-lane blocks (enc_ws) or one 1024-lane
+# block (staged_wsp); 176 keeps the pair kernel's two waves per SIMD.
 BUDGETS = [
-    (r"pair_kernelILi4ELi12ELb0ELb1ELi128ELb1E", 176),   # Encode 12+4 @ 1 MiB (dominant)
-    (r"pair_kernelILi4ELi12ELb0ELb1ELi128ELb0E", 176),   # Encode 12+4 @ 4 KiB
-    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi1024E", 128),  # ReconstOne @ 1 MiB (1024-thread blocks)
-    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi256E", 128),   # ReconstOne @ 4 KiB
+    (r"pair_kernelILi4ELi12ELb0ELb1ELi128ELb1E", 176),   # Encode 12+4 @ 1 MiB (dominant, 170)
+    (r"enc_ws_kernelILi12ELi256EE", 128),                # Encode 12+4 @ 4 KiB (102)
+    (r"enc_ws_kernelILi10ELi256EE", 128),                # Encode 10+4 @ 4 KiB (94)
+    (r"enc_ws_kernelILi8ELi256EE", 128),                 # Encode 8+4 @ 4 KiB (89)
+    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi1024E", 128),  # ReconstOne @ 1 MiB (1024-thread blocks, 94)
+    (r"rows_kernelILi2ELi12ELi4ELb0ELb1ELi256E", 128),   # ReconstOne @ 4 KiB (96)
+    (r"staged_wsp_kernelILi12ELi14ELi2ELi2ELi512EE", 128),  # 2 lost @ 1 MiB (106)
     (r"staged_ws_kernelILi12ELi14ELi2ELi2ELi256ELi1E", 128),
     (r"staged_ws_kernelILi12ELi15ELi1ELi1ELi256ELi1E", 128),
 ]

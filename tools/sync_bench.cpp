@@ -29,6 +29,38 @@ static double cpu_now() {
   return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+// A caller's vects: n buffers of `size` bytes, from ordinary (pageable)
+// memory, or -- g_reg, the "...reg" modes -- from one xrs_host_alloc
+// allocation the library knows as pinned and mapped, so the per-stripe calls
+// skip the CPU copies through staging (the cgo shim's pinned buffer pool).
+static bool g_reg = false;
+struct Bufs {
+  std::vector<std::vector<uint8_t>> own;
+  void* pinned = nullptr;
+  std::vector<uint8_t*> p;
+  Bufs(int n, size_t size, uint8_t fill) {
+    const size_t stride = (size + 63) / 64 * 64;
+    if (g_reg) {
+      pinned = xrs_host_alloc(stride * n);
+      if (!pinned) {
+        std::printf("xrs_host_alloc failed\n");
+        std::fflush(stdout);
+        std::_Exit(4);
+      }
+      for (int i = 0; i < n; ++i) {
+        p.push_back(static_cast<uint8_t*>(pinned) + i * stride);
+        std::memset(p.back(), fill, size);
+      }
+    } else {
+      own.assign(n, std::vector<uint8_t>(size, fill));
+      for (auto& x : own) p.push_back(x.data());
+    }
+  }
+  ~Bufs() {
+    if (pinned) xrs_host_free(pinned);
+  }
+};
+
 // `sync_bench ref`: every sub-benchmark of the reference's xrs_test.go
 // (:471-680) as a per-stripe synchronous call on host vects, one thread, the
 // way `go test -bench` runs it (one stripe, b.N calls), with its SetBytes.
@@ -217,6 +249,11 @@ int main(int argc, char** argv) {
   // `sync_bench SIZE syncmt [THREADS...]`: T threads calling the plain
   // per-stripe xrs_encode / xrs_update on ONE codec (the drop-in call
   // pattern; contended calls go through the codec's auto queue)
+  // "...reg": the same on registered (xrs_host_alloc) vects
+  if (argc > 2 && (std::strcmp(argv[2], "syncmtreg") == 0 || std::strcmp(argv[2], "queuereg") == 0)) {
+    g_reg = true;
+    argv[2][std::strlen(argv[2]) - 3] = 0;
+  }
   if (argc > 2 && std::strcmp(argv[2], "syncmt") == 0) {
     std::vector<int> tl = {1, 8, 32};
     if (argc > 3) {
@@ -230,9 +267,8 @@ int main(int argc, char** argv) {
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t)
           th.emplace_back([&, t] {
-            std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, (uint8_t)t));
-            std::vector<uint8_t*> p;
-            for (auto& x : v) p.push_back(x.data());
+            Bufs b(16, size, static_cast<uint8_t>(t));
+            std::vector<uint8_t*>& p = b.p;
             long n = 0;
             while (!stop.load(std::memory_order_relaxed)) {
               const int rc = upd ? xrs_update(c, p[t % 12], p[(t + 1) % 12], size, t % 12, p.data() + 12, 4)
@@ -253,9 +289,10 @@ int main(int argc, char** argv) {
         const double dt = now() - t0, cpu = cpu_now() - c0;
         const double gib = total * (upd ? 10.0 : 16.0) * size / (1 << 30);
         std::printf("{\"api\": \"%s (per-stripe, shared codec)\", \"vect_bytes\": %zu, \"threads\": %d, "
-                    "\"calls_per_s\": %.0f, \"gibps\": %.3f, \"cpu_cores\": %.2f, "
+                    "\"registered\": %s, \"calls_per_s\": %.0f, \"gibps\": %.3f, \"cpu_cores\": %.2f, "
                     "\"cpu_seconds_per_gib\": %.3f}\n", upd ? "xrs_update" : "xrs_encode", size,
-                    threads, total / dt, gib / dt, cpu / dt, gib > 0 ? cpu / gib : 0.0);
+                    threads, g_reg ? "true" : "false", total / dt, gib / dt, cpu / dt,
+                    gib > 0 ? cpu / gib : 0.0);
         std::fflush(stdout);
       }
     xrs_free(c);
@@ -315,9 +352,8 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
       th.emplace_back([&, t] {
-        std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(size, (uint8_t)t));
-        std::vector<uint8_t*> p;
-        for (auto& x : v) p.push_back(x.data());
+        Bufs b(16, size, static_cast<uint8_t>(t));
+        std::vector<uint8_t*>& p = b.p;
         long n = 0;
         while (!stop.load(std::memory_order_relaxed)) {
           const int rc = upd ? xrs_queue_update(q, p[t % 12], p[(t + 1) % 12], t % 12, p.data() + 12, 4)
@@ -356,12 +392,12 @@ int main(int argc, char** argv) {
     uint64_t st[4] = {0, 0, 0, 0};
     xrs_queue_stats(q, st);
     const double nb = st[0] ? static_cast<double>(st[0]) : 1.0;
-    std::printf("{\"api\": \"%s\", \"vect_bytes\": %zu, \"threads\": %d, "
+    std::printf("{\"api\": \"%s\", \"vect_bytes\": %zu, \"threads\": %d, \"registered\": %s, "
                 "\"stripes_per_s\": %.0f, \"gibps\": %.3f, \"batches\": %llu, "
                 "\"stripes_per_batch\": %.1f, \"run_us_per_batch\": %.1f, "
                 "\"wait_us_per_batch\": %.1f, \"cpu_cores\": %.2f, \"cpu_seconds_per_gib\": %.3f}\n",
                 upd ? "xrs_queue_update" : "xrs_queue_encode",
-                size, threads, total / dt, gib / dt, (unsigned long long)st[0], st[1] / nb,
+                size, threads, g_reg ? "true" : "false", total / dt, gib / dt, (unsigned long long)st[0], st[1] / nb,
                 st[2] / nb / 1e3, st[3] / nb / 1e3, cpu / dt, gib > 0 ? cpu / gib : 0.0);
     std::fflush(stdout);
     if (std::getenv("XRS_QUEUE_DUMP")) {

@@ -118,6 +118,7 @@ def _load():
         "xrs_queue_replace": ([P, PP, IP, I, PP, I], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
+        "xrs_queue_batch_sizes": ([P, ctypes.POINTER(ctypes.c_uint64), I], I),
         "xrs_queue_dump": ([P, ctypes.c_char_p, Z], Z),
         "xrs_group_new": ([I, I, IP, I, ctypes.POINTER(P)], I),
         "xrs_group_free": ([P], None),
@@ -593,6 +594,13 @@ class XRSQueue:
         out = (ctypes.c_uint64 * 4)()
         _raise(_lib.xrs_queue_stats(self._h, out))
         return {"batches": out[0], "stripes": out[1], "run_ns": out[2], "wait_ns": out[3]}
+
+    def batch_sizes(self) -> dict:
+        """{stripes per batch: batches run} since the queue was made
+        (xrs_queue_batch_sizes; counts past 64 stripes are kept as 64)."""
+        out = (ctypes.c_uint64 * 65)()
+        _raise(_lib.xrs_queue_batch_sizes(self._h, out, 65))
+        return {n: int(c) for n, c in enumerate(out) if c}
 
     def dump(self) -> str:
         """The queue's state as text (xrs_queue_dump): per staging batch its

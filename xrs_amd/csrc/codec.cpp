@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "gf256.h"
+#include "hostreg.h"
 #include "xrs_hip.h"
 #include "xrs_plan.h"
 
@@ -1373,6 +1374,37 @@ int run_in_place(const xrs_codec* x, F&& fn) {
 }  // namespace
 
 namespace {
+// Per-stripe calls on caller-registered memory (hostreg.h): when every vect
+// a call touches lies in a range pinned and mapped by xrs_host_alloc /
+// xrs_host_register, the call runs in place -- the kernels read and write the
+// caller's buffers over PCIe through a per-vect pointer table (Layout::table),
+// with no CPU gather into pinned staging and no scatter back.  dev[i] is vect
+// i's device address for the listed vects (0 for the others).
+// XRS_SYNC_REG=0 turns it off (A/B).
+bool reg_vects(uint8_t* const* v, int n, const std::vector<int>& use, size_t size,
+               std::vector<uint64_t>* dev) {
+  static const bool off = [] {
+    const char* e = std::getenv("XRS_SYNC_REG");
+    return e && e[0] == '0';
+  }();
+  if (off) return false;
+  dev->assign(n, 0);
+  for (int i : use) {
+    if (i < 0 || i >= n || !v[i]) return false;
+    const uint64_t a = xrs_detail::host_ranges_device(v[i], size);
+    if (!a) return false;
+    (*dev)[i] = a;
+  }
+  xrs::trace_event("host:sync_in_place");
+  return true;
+}
+
+std::vector<int> iota_vects(int n) {
+  std::vector<int> u(n);
+  for (int i = 0; i < n; ++i) u[i] = i;
+  return u;
+}
+
 // may_queue: a busy codec hands the call to its auto queue (the queue's own
 // fallback for calls it cannot batch comes back here with false).
 int reconst_sync(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, const int* dp_has,
@@ -1391,6 +1423,14 @@ int reconst_sync(const xrs_codec* x, uint8_t* const* vects, int n, size_t size, 
     lk.lock();
   }
   DeviceGuard g(x->device);
+  std::vector<uint64_t> dv;
+  if (size && reg_vects(vects, n, iota_vects(n), size, &dv)) {  // in place, registered memory
+    if ((e = ensure_staging(x, 1))) return e;
+    Written w;
+    e = reconst_impl(x, {nullptr, 0, 0, dv.data()}, size, 1, dp_has, n_has, need, n_need, x->stream, &w);
+    const int es = sync(x);
+    return e ? e : es;
+  }
   Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (int i = 0; i < n && !e; ++i) e = st.in(static_cast<size_t>(i) * size, vects[i], size);
@@ -1623,6 +1663,9 @@ void* xrs_host_alloc(size_t bytes) {
   // group of devices (group.cpp).
   if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
     return nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) xrs_detail::host_ranges_add(p, bytes ? bytes : 1, d);
+  else (void)hipGetLastError();
   return p;
 }
 void* xrs_host_device_pointer(void* host) {
@@ -1635,14 +1678,23 @@ void* xrs_host_device_pointer(void* host) {
   return d;
 }
 void xrs_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  xrs_detail::host_ranges_remove(p);
+  (void)hipHostFree(p);
 }
 int xrs_host_register(void* p, size_t bytes) {
   if (!p || !bytes) return XRS_ERR_INVALID_ARG;
-  return hip_err(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  const int e = hip_err(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  if (e) return e;
+  // the per-stripe calls find the range here without a HIP call (hostreg.h)
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) xrs_detail::host_ranges_add(p, bytes, d);
+  else (void)hipGetLastError();
+  return XRS_OK;
 }
 int xrs_host_unregister(void* p) {
   if (!p) return XRS_ERR_INVALID_ARG;
+  xrs_detail::host_ranges_remove(p);
   return hip_err(hipHostUnregister(p));
 }
 
@@ -1662,6 +1714,13 @@ int xrs_encode(const xrs_codec* x, uint8_t* const* vects, int n, size_t size) {
     lk.lock();
   }
   DeviceGuard g(x->device);
+  std::vector<uint64_t> dv;
+  if (reg_vects(vects, n, iota_vects(n), size, &dv)) {  // in place, registered memory
+    if ((e = ensure_staging(x, 1))) return e;
+    e = encode_impl(x, {nullptr, 0, 0, dv.data()}, size, 1, x->stream);
+    const int es = sync(x);
+    return e ? e : es;
+  }
   Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (int j = 0; j < x->d && !e; ++j) e = st.in(static_cast<size_t>(j) * size, vects[j], size);
@@ -1702,6 +1761,15 @@ int xrs_reconst_one(const xrs_codec* x, uint8_t* const* vects, int n, size_t siz
     lk.lock();
   }
   DeviceGuard g(x->device);
+  std::vector<int> use = {k};
+  for (auto& r : reads) use.push_back(r.first);
+  std::vector<uint64_t> dv;
+  if (reg_vects(vects, n, use, size, &dv)) {  // in place, registered memory
+    if ((e = ensure_staging(x, 1))) return e;
+    e = reconst_one_impl(x, {nullptr, 0, 0, dv.data()}, size, 1, k, x->stream);
+    const int es = sync(x);
+    return e ? e : es;
+  }
   Stage st(x, static_cast<size_t>(n) * size, size);
   if ((e = st.init())) return e;
   for (size_t i = 0; i < reads.size() && !e; ++i) {
@@ -1739,6 +1807,19 @@ int xrs_update(const xrs_codec* x, const uint8_t* old_data, const uint8_t* new_d
     lk.lock();
   }
   DeviceGuard g(x->device);
+  {  // in place, registered memory: rows [0, p) parity, p old, p+1 new
+    std::vector<uint8_t*> v(parity, parity + p);
+    v.push_back(const_cast<uint8_t*>(old_data));
+    v.push_back(const_cast<uint8_t*>(new_data));
+    std::vector<uint64_t> dv;
+    if (reg_vects(v.data(), p + 2, iota_vects(p + 2), size, &dv)) {
+      if ((e = ensure_staging(x, 1))) return e;
+      e = update_impl(x, {dv[p], 0}, {dv[p + 1], 0}, size, row, {nullptr, 0, 0, dv.data()}, 1,
+                      x->stream);
+      const int es = sync(x);
+      return e ? e : es;
+    }
+  }
   // staging rows: [0, p) parity, p old, p+1 new
   const size_t stride = static_cast<size_t>(p + 2) * size;
   Stage st(x, stride, size);
@@ -1772,6 +1853,18 @@ int xrs_replace(const xrs_codec* x, uint8_t* const* data, const int* rows, int n
     lk.lock();
   }
   DeviceGuard g(x->device);
+  {  // in place, registered memory: rows [0, p) parity, [p, p+n) data
+    std::vector<uint8_t*> v(parity, parity + p);
+    v.insert(v.end(), data, data + n);
+    std::vector<uint64_t> dv;
+    if (reg_vects(v.data(), p + n, iota_vects(p + n), size, &dv)) {
+      if ((e = ensure_staging(x, 1))) return e;
+      e = replace_impl(x, {nullptr, 0, 0, dv.data() + p}, rows, n, size, {nullptr, 0, 0, dv.data()}, 1,
+                       x->stream);
+      const int es = sync(x);
+      return e ? e : es;
+    }
+  }
   // staging rows: [0, p) parity, [p, p+n) data
   const size_t stride = static_cast<size_t>(p + n) * size;
   Stage st(x, stride, size);

@@ -852,7 +852,8 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
 }
 
 // Wave-specialised 12+4-style Encode (compile-time source count C, P = 4,
-// 16-byte chunks, halves a multiple of 16 bytes): a block of 2*T lanes works
+// 16-byte chunks; a ragged half ends in an overlapping chunk, as in the pair
+// kernel, with XRS_ENC_WS_RAGGED=1 for A/B): a block of 2*T lanes works
 // on T chunks.  Lanes [0, T) load the C data a-halves, form the four parity
 // a-halves and store them, and leave the piggyback terms (data c rides on
 // parity 1 + c % 3, xrs.go:77-100) in LDS; lanes [T, 2T) load the C data
@@ -868,7 +869,9 @@ __global__ __launch_bounds__(2 * T) void enc_ws_kernel(const PairArgs<4, C, true
   const uint64_t gid = logical_block(a.order) * T + t;
   const bool valid = gid < a.total;
   const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W) + (blane ? a.half : 0);
+  uint64_t o = a.off0 + (gid - stripe * a.chunks) * (4 * W);
+  if (o > a.last) o = a.last;  // ragged end: overlapping last chunk (both roles alike)
+  const uint64_t off = o + (blane ? a.half : 0);
   uint32_t acc[P][W];
   if (valid) {
     uint32_t x[C][W];
@@ -1266,6 +1269,42 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P
     const uint64_t dq = row_addr(a.dst[q], stripe, off);
     st<VEC>(pa[q], dq, nb);
     st<VEC>(pb[q], dq + a.half, nb);
+  }
+}
+
+// ============================================================ copy kernel
+// The batching queue's gather / scatter (xrs_plan.h CopyPlan): block (x, y, z)
+// moves chunks [256x, 256x + 256) of 16 bytes of piece y of stripe z between
+// the caller's row (its address from the stripe's row table, in registered
+// host memory read over PCIe) and the compact device staging.  A piece of 16
+// bytes or more ends in one overlapping 16-byte chunk (the copy is pure, so
+// the overlap rewrites equal bytes); a shorter one is copied byte by byte.
+// Any alignment: MI355X runs unaligned dwordx4 accesses (kernels above).
+constexpr int kCopyBlock = 256;
+
+struct CopyArgs {
+  CopyPiece piece[kMaxPieces];
+  const uint64_t* tab;
+  uint64_t nrows;
+  uint64_t stage, stripe_bytes, row_bytes;
+  uint32_t gather;
+};
+
+__global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CopyArgs a) {
+  const CopyPiece pc = a.piece[blockIdx.y];
+  const uint64_t stripe = blockIdx.z;
+  const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * kCopyBlock + threadIdx.x) * 16;
+  if (c >= pc.len) return;
+  const uint64_t row = a.tab[stripe * a.nrows + pc.row] + pc.off;
+  const uint64_t stg = a.stage + stripe * a.stripe_bytes + pc.row * a.row_bytes + pc.off;
+  const uint64_t src = a.gather ? row : stg, dst = a.gather ? stg : row;
+  if (pc.len >= 16) {
+    const uint64_t o = c + 16 > pc.len ? pc.len - 16 : c;
+    *reinterpret_cast<gu32x4*>(dst + o) = *reinterpret_cast<const gu32x4*>(src + o);
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i)
+      if (i < pc.len) reinterpret_cast<gu8*>(dst)[i] = reinterpret_cast<const gu8*>(src)[i];
   }
 }
 
@@ -1918,11 +1957,15 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
     // +8.8 / +1.9%), not for 14+4, 16+4 (-1.9..+1.5%) or 20+4 (-13..-19%,
     // 134 VGPRs): profiles/r04_encws_codecs.log.  XRS_ENC_WS forces it for
     // every d+4 compile-time shape (A/B); =0 turns it off, =128 / 256 / 512
-    // sets the block size (12+4; 256 for the others).
+    // sets the block size (12+4; 256 for the others), any other value forces
+    // it on with 256 chunks per block.
     const char* ew = std::getenv("XRS_ENC_WS");
     const bool ws_on = (ew && *ew) ? ew[0] != '0' : (C <= 12 && p.half <= (128u << 10));
-    if (ws_on && p.half % 16 == 0) {
-      const int T = (C == 12 && ew && *ew) ? std::atoi(ew) : 256;
+    const char* rg = std::getenv("XRS_ENC_WS_RAGGED");
+    if (ws_on && (p.half % 16 == 0 || (rg && rg[0] == '1'))) {
+      int T = 256;  // the block size launched below, which also sets the grid
+      if (C == 12 && ew && (std::strcmp(ew, "128") == 0 || std::strcmp(ew, "512") == 0))
+        T = std::strcmp(ew, "128") == 0 ? 128 : 512;
       const uint64_t tb = (a.total + T - 1) / T;
       if (tb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
       a.order = block_order(Shape::kPair, VEC, p.half, tb, T);
@@ -2260,6 +2303,10 @@ std::atomic<bool> g_trace{false};
 std::mutex g_trace_mu;
 std::vector<std::pair<std::string, uint64_t>> g_trace_log;
 
+void trace_event(const char* name) {
+  if (g_trace.load(std::memory_order_relaxed)) trace_note(name);
+}
+
 void trace_kernels(bool on) {
   std::lock_guard<std::mutex> g(g_trace_mu);
   if (on) g_trace_log.clear();
@@ -2336,6 +2383,38 @@ int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
   return split_launch(p0, p0.half, al, [s](const UpdRowsPlan& p, bool vec) {
     return vec ? launch_update_rows_p<true>(p, s) : launch_update_rows_p<false>(p, s);
   });
+}
+
+int launch_copy(const CopyPlan& p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.npieces > static_cast<uint32_t>(kMaxPieces) || !p.tab || !p.stage) return static_cast<int>(hipErrorInvalidValue);
+  if (p.npieces == 0 || p.n_stripes == 0) return 0;
+  CopyArgs a;
+  std::memset(&a, 0, sizeof(a));
+  uint64_t maxlen = 0;
+  for (uint32_t i = 0; i < p.npieces; ++i) {
+    if (p.piece[i].row >= p.nrows) return static_cast<int>(hipErrorInvalidValue);
+    a.piece[i] = p.piece[i];
+    maxlen = std::max<uint64_t>(maxlen, p.piece[i].len);
+  }
+  a.nrows = p.nrows;
+  a.stripe_bytes = p.stripe_bytes;
+  a.row_bytes = p.row_bytes;
+  a.gather = p.gather ? 1u : 0u;
+  const uint64_t xb = (maxlen + 16 * kCopyBlock - 1) / (16 * kCopyBlock);
+  if (xb == 0 || xb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  constexpr uint64_t kMaxZ = 65535;  // grid z limit: stripes in chunks
+  for (uint64_t s0 = 0; s0 < p.n_stripes; s0 += kMaxZ) {
+    const uint64_t nz = std::min(kMaxZ, p.n_stripes - s0);
+    a.tab = reinterpret_cast<const uint64_t*>(p.tab) + s0 * p.nrows;
+    a.stage = p.stage + s0 * p.stripe_bytes;
+    XRS_LAUNCH(copy_kernel, dim3(static_cast<unsigned>(xb), p.npieces, static_cast<unsigned>(nz)),
+               dim3(kCopyBlock), s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return 0;
 }
 #endif  // XRS_HAS_PART(3)
 

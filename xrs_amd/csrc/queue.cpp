@@ -56,7 +56,9 @@
 #include <thread>
 #include <vector>
 
+#include "hostreg.h"
 #include "xrs_hip.h"
+#include "xrs_plan.h"
 
 namespace xrs_detail {
 int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
@@ -118,6 +120,13 @@ struct Batch {
   uint8_t* dev = nullptr;
   int32_t* rows = nullptr;      // pinned, mapped: Update's data row per slot
   int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
+  // Row tables (pinned, mapped; nrows per slot): the device address of each
+  // staged row's bytes -- the caller's own vect when it lies in registered
+  // memory (hostreg.h), else the slot's row in `host`.  A batch with any
+  // registered slot runs gather kernel -> op on `dev` -> scatter kernel.
+  uint64_t* tab = nullptr;
+  uint64_t* tab_dev = nullptr;
+  std::vector<xrs::CopyPiece> pin, pout;  // the batch's pieces (one layout per key)
   hipStream_t stream = nullptr;
   volatile uint32_t* flag = nullptr;  // pinned host word the stream writes `launches` to
   uint32_t* flag_dev = nullptr;
@@ -132,6 +141,7 @@ struct Batch {
   // lock-free: slots staged / slots released, and the completion word (+1
   // when the batch's results are in staging; err and n are written first)
   std::atomic<uint32_t> filled{0}, released{0}, done{0};
+  std::atomic<uint32_t> n_reg{0};  // slots whose vects are all in registered memory
   size_t n = 0;  // slots of the closed batch
   int err = 0;
 };
@@ -143,6 +153,8 @@ struct xrs_queue {
   int d = 0, p = 0, device = -1;
   size_t size = 0, stripe_bytes = 0, max_batch = 1, zc_max = 0;
   size_t bo = 0;  // staged stripes start at the odd-size base offset (b-halves aligned)
+  size_t nrows = 0;     // staged rows per stripe (stripe_bytes / size)
+  bool reg_ok = false;  // row tables allocated: registered callers skip the copies
   std::chrono::microseconds max_wait{50};
   Batch b[kBatches];
   uint32_t* flags = nullptr;  // pinned, mapped: kFlagStride words per batch
@@ -155,6 +167,10 @@ struct xrs_queue {
   // (launch to completion seen) and queueing time (open to launch) summed
   // over batches, in ns
   uint64_t st_batches = 0, st_stripes = 0, st_run_ns = 0, st_wait_ns = 0;
+  // batches run by stripe count (index n: n stripes; the last bucket: more)
+  static constexpr int kHist = 65;
+  static constexpr int kMaxRows = 258;  // staged rows per stripe: max(d + p, p + 2) <= 258
+  uint64_t st_hist[kHist] = {};
   std::mutex mu;
   std::condition_variable cv_work, cv_free, cv_comp;
   std::thread worker[kMaxWorkers], completer;
@@ -211,12 +227,34 @@ int xrs_queue::launch(Batch& bt) {
                             : upd || rec || rep ? 0 : static_cast<size_t>(bt.key - 1) * size;
   const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
                                           : rec ? static_cast<size_t>(d + p) * size : size;
-  const bool zc = bt.host_dev && n * stripe_bytes <= zc_max;
+  // Registered callers: gather their rows into device staging, run, scatter
+  // the outputs back, all on the GPU (XRS_QUEUE_REG=0: never).
+  const bool table = reg_ok && bt.n_reg.load(std::memory_order_acquire) > 0;
+  const bool zc = !table && bt.host_dev && n * stripe_bytes <= zc_max;
   uint8_t* base = (zc ? bt.host_dev : bt.dev) + bo;
   uint8_t *hst = bt.host + bo, *dst = bt.dev + bo;
+  auto copy = [&](const std::vector<xrs::CopyPiece>& pcs, bool gather) {
+    xrs::CopyPlan cp;
+    std::memset(&cp, 0, sizeof(cp));
+    cp.tab = reinterpret_cast<uint64_t>(bt.tab_dev);
+    cp.nrows = static_cast<uint32_t>(nrows);
+    cp.stage = reinterpret_cast<uint64_t>(dst);
+    cp.stripe_bytes = stripe_bytes;
+    cp.row_bytes = size;
+    cp.n_stripes = n;
+    cp.gather = gather;
+    for (size_t i0 = 0; i0 < pcs.size(); i0 += xrs::kMaxPieces) {
+      cp.npieces = static_cast<uint32_t>(std::min<size_t>(xrs::kMaxPieces, pcs.size() - i0));
+      for (uint32_t i = 0; i < cp.npieces; ++i) cp.piece[i] = pcs[i0 + i];
+      if (xrs::launch_copy(cp, bt.stream) != 0) return XRS_ERR_HIP;
+    }
+    return XRS_OK;
+  };
   int e = 0;
-  if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
-                              n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
+  if (table)
+    e = copy(bt.pin, true);
+  else if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
+                                   n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
   if (!e) {
     if (enc)
@@ -237,9 +275,11 @@ int xrs_queue::launch(Batch& bt) {
       e = xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n, bt.key - 1,
                                       bt.stream);
   }
-  if (!e && !zc &&
-      hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
-                       hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
+  if (!e && table)
+    e = copy(bt.pout, false);
+  else if (!e && !zc &&
+           hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
+                            hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
     e = XRS_ERR_HIP;
   if (!e && hipStreamWriteValue32(bt.stream, bt.flag_dev, ++bt.launches, 0) != hipSuccess)
     e = XRS_ERR_HIP;
@@ -257,6 +297,7 @@ void xrs_queue::finish(int i, int err) {
     --in_flight;
     ++st_batches;
     st_stripes += bt.n;
+    ++st_hist[std::min<size_t>(bt.n, kHist - 1)];
     st_run_ns += ns_since(bt.launched);
     cv_work.notify_one();  // a launcher may wait for in_flight < max_inflight
   }
@@ -340,11 +381,13 @@ void xrs_queue::complete() {
     // checks (which are not free: spinning on hipStreamQuery saw an empty
     // kernel done 5-9 us later than its host word, r03_queue_latency_probe).
     auto idle = Clock::now();
+    bool slept = false;
     for (uint32_t it = 1;; ++it) {
       uint32_t bits = inflight_bits.load(std::memory_order_acquire);
       if (!bits) break;
       bool any = false;
-      const bool poll = (it & 1023) == 0;
+      const bool poll = slept || (it & 1023) == 0;
+      slept = false;
       for (uint32_t m = bits; m; m &= m - 1) {
         const int i = __builtin_ctz(m);
         Batch& bt = b[i];
@@ -365,9 +408,12 @@ void xrs_queue::complete() {
       if (any) {
         idle = Clock::now();
       } else if (ns_since(idle) > comp_spin_ns) {
-        // a long batch (large stripes over PCIe): poll every 20 us instead of
-        // burning a core (adds at most 20 us to a batch that ran > 200 us)
+        // a long batch (large stripes over PCIe): sleep between polls instead
+        // of burning a core.  A 20 us sleep lasts 70-80 us under Linux's
+        // default 50 us timer slack, which a batch that already ran > 200 us
+        // can absorb; the stuck-stream check runs on every sleeping pass.
         std::this_thread::sleep_for(std::chrono::microseconds(20));
+        slept = true;
       } else {
         _mm_pause();
       }
@@ -380,6 +426,17 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   auto same_pattern = [&](const Batch& bt) {
     return !has || (bt.pat_has == *has && bt.pat_need == *need);
   };
+  // Device address of each staged row's vect when every vect of the call lies
+  // in registered host memory (hostreg.h): then no copy on this thread.
+  uint64_t regdev[xrs_queue::kMaxRows];
+  bool reg = reg_ok;
+  for (const auto* ps : {&in, &out})
+    for (const Piece& pc : *ps)
+      if (reg) {
+        const uint64_t a = xrs_detail::host_ranges_device(pc.host, size);
+        reg = a != 0 && pc.row >= 0 && static_cast<size_t>(pc.row) < nrows;
+        if (reg) regdev[pc.row] = a;
+      }
   Batch* bp;
   size_t slot;
   uint32_t seq;
@@ -410,6 +467,15 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       nb.filled.store(0, std::memory_order_relaxed);
       nb.released.store(0, std::memory_order_relaxed);
       nb.err = 0;
+      nb.n_reg.store(0, std::memory_order_relaxed);
+      nb.pin.clear();
+      nb.pout.clear();
+      for (const Piece& pc : in)
+        nb.pin.push_back({static_cast<uint32_t>(pc.row), static_cast<uint32_t>(pc.off),
+                          static_cast<uint32_t>(pc.len)});
+      for (const Piece& pc : out)
+        nb.pout.push_back({static_cast<uint32_t>(pc.row), static_cast<uint32_t>(pc.off),
+                           static_cast<uint32_t>(pc.len)});
       nb.opened = Clock::now();
       if (has) {
         nb.pat_has = *has;
@@ -426,8 +492,17 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   Batch& bt = *bp;
   uint8_t* st = bt.host + bo + slot * stripe_bytes;
   if (row >= 0) bt.rows[slot] = row;
-  for (const Piece& pc : in)
-    std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
+  if (reg_ok) {
+    uint64_t* tb = bt.tab + slot * nrows;
+    const uint64_t sd = reinterpret_cast<uint64_t>(bt.host_dev + bo + slot * stripe_bytes);
+    for (const auto* ps : {&in, &out})
+      for (const Piece& pc : *ps)
+        tb[pc.row] = reg ? regdev[pc.row] : sd + static_cast<uint64_t>(pc.row) * size;
+    if (reg) bt.n_reg.fetch_add(1, std::memory_order_relaxed);
+  }
+  if (!reg)
+    for (const Piece& pc : in)
+      std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
   bt.filled.fetch_add(1, std::memory_order_release);
   if (timer) {
     // the timer policy's launcher may be asleep on a batch that is now staged
@@ -440,7 +515,7 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   // caller may free the batch and a new submit() reopen it (n = 0).
   const size_t n_slots = bt.n;
   const int err = bt.err;
-  if (!err)
+  if (!err && !reg)
     for (const Piece& pc : out)
       std::memcpy(pc.host + pc.off, st + static_cast<size_t>(pc.row) * size + pc.off, pc.len);
   if (bt.released.fetch_add(1, std::memory_order_acq_rel) + 1 == n_slots) {
@@ -472,6 +547,7 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   // xrs_batch_layout's base offset: with an odd half (size % 32 != 0) every
   // staged b-half is as aligned as in a recommended device batch
   q->bo = (16 - (size / 2) % 16) % 16;
+  q->nrows = q->stripe_bytes / size;
   q->max_batch = std::max<size_t>(
       1, std::min(max_batch_stripes ? max_batch_stripes : SIZE_MAX, kMaxBatchBytes / q->stripe_bytes));
   q->max_wait = std::chrono::microseconds(max_wait_us);
@@ -488,6 +564,8 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
   q->timer = pv && std::strcmp(pv, "timer") == 0;
   const char* nv = std::getenv("XRS_QUEUE_SPIN_NS");
   if (nv && *nv) q->spin_ns = std::strtoull(nv, nullptr, 0);
+  const char* rv = std::getenv("XRS_QUEUE_REG");
+  q->reg_ok = !(rv && rv[0] == '0');
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
@@ -516,6 +594,17 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
       break;
     }
     bt.rows_dev = static_cast<int32_t*>(dp);
+    // row tables for registered callers (at most 16 MiB per batch, else the
+    // queue copies every call through `host`; XRS_QUEUE_REG=0: always)
+    const size_t tb = q->max_batch * q->nrows * sizeof(uint64_t);
+    if (q->reg_ok && tb <= (16u << 20) &&
+        hipHostMalloc(reinterpret_cast<void**>(&bt.tab), tb, hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer(&dp, bt.tab, 0) == hipSuccess && bt.host_dev) {
+      bt.tab_dev = static_cast<uint64_t*>(dp);
+    } else {
+      (void)hipGetLastError();
+      q->reg_ok = false;
+    }
   }
   if (prev >= 0) (void)hipSetDevice(prev);
   if (e) {
@@ -557,6 +646,7 @@ void xrs_queue_free(xrs_queue* q) {
     if (bt.dev) (void)hipFree(bt.dev);
     if (bt.host) (void)hipHostFree(bt.host);
     if (bt.rows) (void)hipHostFree(bt.rows);
+    if (bt.tab) (void)hipHostFree(bt.tab);
   }
   if (q->flags) (void)hipHostFree(q->flags);
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -704,6 +794,14 @@ int xrs_queue_stats(xrs_queue* q, uint64_t out[4]) {
   out[1] = q->st_stripes;
   out[2] = q->st_run_ns;
   out[3] = q->st_wait_ns;
+  return XRS_OK;
+}
+
+int xrs_queue_batch_sizes(xrs_queue* q, uint64_t* counts, int cap) {
+  if (!q || !counts || cap < 1) return XRS_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(q->mu);
+  for (int i = 0; i < cap; ++i) counts[i] = 0;
+  for (int n = 0; n < xrs_queue::kHist; ++n) counts[std::min(n, cap - 1)] += q->st_hist[n];
   return XRS_OK;
 }
 

@@ -325,6 +325,52 @@ def test_reconst_persistent_concurrent_streams(rng, monkeypatch):
             assert np.array_equal(got[st], want[st]), st
 
 
+def test_reconst_persistent_counter_slots_reused(rng, monkeypatch):
+    """320 persistent launches, 80 on each of four streams in two waves of at
+    most 160 in flight, more than the 256 tile-counter slots of the device's
+    ring (kernels.hip tile_counters): each launch's last block resets its
+    slot, so every launch runs the persistent kernel (none falls back for want
+    of a free slot) and every
+    buffer equals the oracle after the same 80 calls (a repeated Reconst
+    toggles the retrieveRS side effect, xrs.go:305-320, so the oracle replays
+    every call)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("XRS_WSP", "512")
+    monkeypatch.setenv("XRS_WSP_GRID", "8")
+    size, n, calls = 4096, 40, 80
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
+    o.encode_batch(host, size, n)
+    lost = [2, 7]
+    h = host.copy()
+    h[:, lost] = 0x5A
+    has = [i for i in range(D + P) if i not in lost]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    ts = [torch.from_numpy(h).cuda() for _ in streams]
+    torch.cuda.synchronize()
+    xrs_amd.trace_kernels(True)
+    try:
+        for c in range(calls):
+            for t, st in zip(ts, streams):
+                x.reconst_batched(t.data_ptr(), size, size, (D + P) * size, n, has, lost,
+                                  st.cuda_stream)
+            if c % 40 == 39:  # at most 160 launches queued: the slots are reused,
+                torch.cuda.synchronize()  # never all held at once
+    finally:
+        xrs_amd.trace_kernels(False)
+    assert xrs_amd.traced_kernels() == {"staged_wsp_kernel<12, 14, 2, 2, 512>": 4 * calls}
+    want = []
+    for st in range(n):
+        w = [h[st, i].copy() for i in range(D + P)]
+        for _ in range(calls):
+            o.reconst(w, has, lost)
+        want.append(np.stack(w))
+    for t in ts:
+        got = t.cpu().numpy()
+        for st in range(n):
+            assert np.array_equal(got[st], want[st]), st
+
+
 @pytest.mark.parametrize("ws", ["", "0", "rt"])
 @pytest.mark.parametrize("d,p", [(10, 4), (16, 4), (6, 3), (12, 4), (15, 5), (8, 4), (14, 4),
                                  (10, 2)])

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5, first GPU call: the new tests (queue coalescing, registered-memory
-# per-stripe calls) and smoke, the per-stripe rates with and without
+# per-stripe calls, persistent-kernel counter slots) and smoke, the
+# persistent kernel's per-call cost (item 6), the per-stripe rates with and without
 # registered vects, the staged large-half investigation
 # (item 2: rates, then rocprofv3 --pmc passes) and the parked ragged-half
 # Encode A/B (item 5).
@@ -11,6 +12,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
     tests/test_kernel_resources.py tests/test_gpu_registered.py \
     "tests/test_gpu_queue.py::test_queue_coalesces_barrier_released_callers" \
+    "tests/test_gpu_edge.py::test_reconst_persistent_counter_slots_reused" \
+    "tests/test_gpu_edge.py::test_reconst_persistent_concurrent_streams" \
+    "tests/test_gpu_edge.py::test_reconst_batched_persistent_vs_oracle" \
     -s > gpurun_out/r05_first_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r05_first_tests.log; grep "queue:" gpurun_out/r05_first_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05_smoke.log 2>&1
@@ -23,6 +27,8 @@ for mode in syncmt syncmtreg; do
   timeout -k 10 120 ./tools/sync_bench 4096 $mode 1 8 32 >> gpurun_out/r05_sync_bench.log 2>&1 || { echo "sync_bench $mode rc=$?"; tail gpurun_out/r05_sync_bench.log; exit 1; }
 done
 grep '^{' gpurun_out/r05_sync_bench.log
+timeout -k 10 240 python -u tools/wsp_call_overhead.py > gpurun_out/r05_wsp_overhead.log 2>&1
+rc=$?; grep n= gpurun_out/r05_wsp_overhead.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python -u tools/staged_big_cases.py > gpurun_out/r05_staged_big.log 2>&1
 rc=$?; grep '^{' gpurun_out/r05_staged_big.log; [ $rc -eq 0 ] || { tail -20 gpurun_out/r05_staged_big.log; exit $rc; }
 export CASES=A,C,D,E,F,G,H

@@ -1047,7 +1047,13 @@ int xrs_new(int data_num, int parity_num, xrs_codec** out) {
   int count = 0;
   if (dev >= 0 && (hipGetDeviceCount(&count) != hipSuccess || count <= 0)) dev = -1;
   x->device = dev;
-  if (dev >= 0) (void)xrs::zero_rows(dev);  // Encode padding rows: never allocated in a launch
+  // Encode padding rows and the persistent kernel's tile counters of the
+  // codec's device, made here so a launch on it never allocates (a launch on
+  // another device's stream makes that device's on first use)
+  if (dev >= 0) {
+    (void)xrs::zero_rows(dev);
+    (void)xrs::tile_counters(dev);
+  }
   *out = x;
   return XRS_OK;
 }

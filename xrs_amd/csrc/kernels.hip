@@ -955,9 +955,14 @@ __device__ __forceinline__ void ktabs(GfTab (&t)[R], const XRS_KC GfTab* src) {
   for (int r = 0; r < R; ++r) t[r] = kld(src[r]);
 }
 
+// ctr: the launch's counter slot (ctr[0] hands out tiles, ctr[1] counts the
+// blocks done) and busy, the slot's host word (tile_counters below): the last
+// block out resets both counters and then clears busy, so the slot is free
+// for the next launch on any stream without a host-side reset.
 template <int ND, int NB, int NL, int NN, int T>
 __global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, NN, true> a,
-                                                            const uint32_t ntiles, uint32_t* ctr) {
+                                                            const uint32_t ntiles, uint32_t* ctr,
+                                                            uint32_t* busy) {
   using Args = StagedArgs<NL, NN, true>;
   constexpr int W = 4;
   __shared__ uint4 xfer[2][kStOut + NN][T];
@@ -1024,6 +1029,15 @@ __global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, 
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
       v = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
+    }
+    // This block takes no more tiles.  The last block to get here resets the
+    // slot: every block's tile atomics are ordered before its arrival (acq_rel
+    // at agent scope), so nothing touches ctr[0] after the reset.
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }
@@ -1470,43 +1484,81 @@ int cu_count(hipStream_t s) {
 // Persistent wave-specialised staged kernel (staged_wsp_kernel): one block
 // of 2*T lanes per compute unit (XRS_WSP_PER_CU: more, A/B; XRS_WSP_GRID: an
 // exact block count, so tests give every block many tiles), K = the tiles of
-// one half-vect (XRS_WS_ORDER overrides).  The tile counter is this launch's
-// own (stream-ordered allocation, so launches on other streams never share
-// it).  Returns kNotLaunched when it cannot be allocated; the caller then
-// runs the one-shot kernel.
+// one half-vect (XRS_WS_ORDER overrides).  The tile counter is a slot of the
+// launch stream's device's ring (tile_counters), claimed here and released by
+// the kernel itself.  Returns kNotLaunched when no slot is free; the caller
+// then runs the one-shot kernel.
 constexpr int kNotLaunched = -1;
 
-// A memory pool of the library's own for those counters, keeping what it
-// reserves (release threshold: never), so a launch's counter costs no
-// driver allocation; nullptr (the device's default pool) if it cannot be made.
-hipMemPool_t counter_pool(hipStream_t s) {
+// Tile counters of the persistent kernels, per device: kCtrSlots slots of two
+// counters (one 128-B line each) in device memory, zero when free, and one
+// pinned host word per slot, 1 while a launch holds it.  A launch claims a
+// slot with a host compare-and-swap; the kernel's last block resets the
+// counters and clears the word (a system-scope release store), so a slot is
+// never shared by two launches in flight, whatever their streams, and a
+// launch costs no allocation, memset or free (round 4's stream-ordered
+// counter cost 2-7 us per synchronous call, profiles/r04_wsp_overhead.log).
+constexpr int kCtrSlots = 256;
+constexpr int kCtrLine = 32;   // uint32 per counter slot (128 B)
+constexpr int kBusyLine = 16;  // uint32 per host word (64 B)
+struct CtrRing {
+  uint32_t* ctr = nullptr;       // device memory, kCtrSlots * kCtrLine words
+  uint32_t* busy = nullptr;      // pinned host memory, kCtrSlots * kBusyLine words
+  uint32_t* busy_dev = nullptr;  // its device address
+  std::atomic<uint32_t> next{0};
+};
+
+CtrRing* ctr_ring(int dev) {
   static std::mutex mu;
-  static hipMemPool_t pools[64] = {};
+  static CtrRing* rings[64] = {};
   static bool tried[64] = {};
-  int dev = 0;
-  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= 64) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
+  if (dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> g(mu);
   if (!tried[dev]) {
     tried[dev] = true;
-    hipMemPoolProps pp;
-    std::memset(&pp, 0, sizeof(pp));
-    pp.allocType = hipMemAllocationTypePinned;
-    pp.handleTypes = hipMemHandleTypeNone;
-    pp.location.type = hipMemLocationTypeDevice;
-    pp.location.id = dev;
-    hipMemPool_t pool = nullptr;
-    if (hipMemPoolCreate(&pool, &pp) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-      pools[dev] = pool;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    auto* r = new CtrRing();
+    hipStream_t z = nullptr;
+    void* dp = nullptr;
+    bool ok = hipMalloc(reinterpret_cast<void**>(&r->ctr), kCtrSlots * kCtrLine * sizeof(uint32_t)) == hipSuccess;
+    // zeroed on a private stream: no null-stream barrier against the user's work
+    ok = ok && hipStreamCreateWithFlags(&z, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMemsetAsync(r->ctr, 0, kCtrSlots * kCtrLine * sizeof(uint32_t), z) == hipSuccess &&
+         hipStreamSynchronize(z) == hipSuccess;
+    if (z) (void)hipStreamDestroy(z);
+    ok = ok && hipHostMalloc(reinterpret_cast<void**>(&r->busy), kCtrSlots * kBusyLine * sizeof(uint32_t),
+                             hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipHostGetDevicePointer(&dp, r->busy, 0) == hipSuccess;
+    if (ok) {
+      std::memset(r->busy, 0, kCtrSlots * kBusyLine * sizeof(uint32_t));
+      r->busy_dev = static_cast<uint32_t*>(dp);
+      rings[dev] = r;
     } else {
       (void)hipGetLastError();
+      if (r->ctr) (void)hipFree(r->ctr);
+      if (r->busy) (void)hipHostFree(r->busy);
+      delete r;
     }
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
   }
-  return pools[dev];
+  return rings[dev];
+}
+
+// A free slot of ring r, now held by the caller (its busy word set), or -1.
+int claim_slot(CtrRing* r) {
+  for (int i = 0; i < kCtrSlots; ++i) {
+    const uint32_t s = r->next.fetch_add(1, std::memory_order_relaxed) % kCtrSlots;
+    uint32_t expect = 0;
+    if (__atomic_compare_exchange_n(r->busy + s * kBusyLine, &expect, 1u, false, __ATOMIC_ACQ_REL,
+                                    __ATOMIC_ACQUIRE))
+      return static_cast<int>(s);
+  }
+  return -1;
 }
 
 template <int NL, int NN, int T>
@@ -1526,27 +1578,27 @@ int launch_staged_wsp(StagedArgs<NL, NN, true> a, const StagedPlan& p, hipStream
   grid = std::min<uint64_t>(tiles, grid);
   const dim3 g(static_cast<unsigned>(grid));
   const uint32_t nt = static_cast<uint32_t>(tiles);
-  uint32_t* ctr = nullptr;
-  const hipMemPool_t pool = counter_pool(stream);
-  const hipError_t ae =
-      pool ? hipMallocFromPoolAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), pool, stream)
-           : hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(uint32_t), stream);
-  if (ae != hipSuccess) {
+  int dev = -1;
+  if (hipStreamGetDevice(stream, &dev) != hipSuccess) {
     (void)hipGetLastError();
     return kNotLaunched;
   }
-  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), stream);
-  if (e == hipSuccess) {
-    if (p.nb == 12)
-      XRS_LAUNCH((staged_wsp_kernel<12, 12, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
-    else if (p.nb == 13)
-      XRS_LAUNCH((staged_wsp_kernel<12, 13, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
-    else
-      XRS_LAUNCH((staged_wsp_kernel<12, 14, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr);
-    e = hipGetLastError();
-  }
-  const hipError_t f = hipFreeAsync(ctr, stream);
-  return static_cast<int>(e != hipSuccess ? e : f);
+  CtrRing* ring = ctr_ring(dev);
+  const int slot = ring ? claim_slot(ring) : -1;
+  if (slot < 0) return kNotLaunched;
+  uint32_t* ctr = ring->ctr + slot * kCtrLine;
+  uint32_t* busy = ring->busy_dev + slot * kBusyLine;
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  if (p.nb == 12)
+    XRS_LAUNCH((staged_wsp_kernel<12, 12, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr, busy);
+  else if (p.nb == 13)
+    XRS_LAUNCH((staged_wsp_kernel<12, 13, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr, busy);
+  else
+    XRS_LAUNCH((staged_wsp_kernel<12, 14, NL, NN, T>), g, dim3(2 * T), stream, a, nt, ctr, busy);
+  const hipError_t e = hipGetLastError();
+  // not launched: the kernel will not release the slot, so release it here
+  if (e != hipSuccess) __atomic_store_n(ring->busy + slot * kBusyLine, 0u, __ATOMIC_RELEASE);
+  return static_cast<int>(e);
 }
 
 // Other codecs' clean lost-data patterns (na = nd = ND, nb = ND..ND+2: the
@@ -1739,20 +1791,24 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // vects +2.9 / -0.1 / +4.2 / +2.6%; 2 / 4 / 8 MiB -1.8 / +0.7 / -14.7%,
       // so larger halves keep the one-shot kernel; 3 lost -2..-4% and
       // 256-chunk tiles -5..-21%, profiles/r04_wsp_sizes.log).
-      // Only launches of at least 16 tiles per CU (64 stripes of 1 MiB):
-      // the per-launch counter (alloc from counter_pool + memset + free)
-      // costs 2-7 us per synchronous call, which smaller launches do not win
-      // back (tools/wsp_call_overhead.py, profiles/r04_wsp_overhead.log:
-      // 4 / 16 / 64 / 256 stripes of 1 MiB +7.0 / +2.4 / -4.5 / -34 us).
-      // XRS_WSP=0 turns it off, =512 / =256 forces it (A/B, tests).
+      // Only launches of at least XRS_WSP_MIN_TILES (per CU, default 16:
+      // 64 stripes of 1 MiB): the round-4 per-launch counter (stream-ordered
+      // alloc + memset + free) cost 2-7 us per synchronous call, which smaller
+      // launches did not win back (tools/wsp_call_overhead.py,
+      // profiles/r04_wsp_overhead.log: 4 / 16 / 64 / 256 stripes of 1 MiB
+      // +7.0 / +2.4 / -4.5 / -34 us); the counter is now a self-resetting
+      // slot (tile_counters).  XRS_WSP=0 turns it off, =512 / =256 forces it
+      // (A/B, tests).
       const char* pv = std::getenv("XRS_WSP");
       const bool wsp_off = pv && pv[0] == '0';
+      const char* mt = std::getenv("XRS_WSP_MIN_TILES");
+      const uint64_t min_tiles = (mt && *mt) ? std::strtoull(mt, nullptr, 10) : uint64_t(16);
       int wsp = kNotLaunched;
       if (pv && std::strcmp(pv, "256") == 0) wsp = launch_staged_wsp<NL, NN, 256>(a, p, stream);
       else if (pv && std::strcmp(pv, "512") == 0) wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
       else if (NL == 2 && !wsp_off && (!wv || !*wv || std::strcmp(wv, "rt") == 0) &&
                p.half >= (256u << 10) && p.half <= (768u << 10) &&
-               a.total >= uint64_t(512) * 16 * static_cast<uint64_t>(cu_count(stream)))
+               a.total >= uint64_t(512) * min_tiles * static_cast<uint64_t>(cu_count(stream)))
         wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
       if (wsp != kNotLaunched) return wsp;
       if (!wv || !*wv || std::strcmp(wv, "rt") == 0) {
@@ -2346,6 +2402,8 @@ int launch_pair(const PairPlan& p0, void* stream) {
 #endif  // XRS_HAS_PART(1)
 
 #if XRS_HAS_PART(2)
+bool tile_counters(int dev) { return ctr_ring(dev) != nullptr; }
+
 int launch_staged(const StagedPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStB || p0.nl < 0 ||

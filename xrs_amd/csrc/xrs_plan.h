@@ -168,7 +168,14 @@ void trace_event(const char* name);
 // Device address of the zero rows that pad an Encode to a compile-time
 // source count on device `dev` (allocated and zeroed on first call for that
 // device, never freed: a launch in flight may read it), or 0.  xrs_new calls
-// it for the codec's device so the launch path never allocates.
+// it for the codec's device, so a launch there never allocates; a launch on
+// another device's stream makes that device's rows on first use.
 uint64_t zero_rows(int dev);
+// Makes device `dev`'s ring of tile-counter slots for the persistent staged
+// kernel (kernels.hip ctr_ring: on first call for that device, never freed);
+// false if it cannot be made (the one-shot kernels run instead).  xrs_new
+// calls it for the codec's device; a launch on another device's stream makes
+// that device's ring on first use.
+bool tile_counters(int dev);
 
 }  // namespace xrs

@@ -247,6 +247,13 @@ class Queue {
                                        static_cast<int>(p.size())),
                       row);
   }
+  // Batches run so far by stripe count (xrs_queue_batch_sizes): element n =
+  // batches of n stripes, the last element = batches of 64 or more.
+  std::vector<uint64_t> BatchSizes() const {
+    std::vector<uint64_t> c(65, 0);
+    if (xrs_queue_batch_sizes(q_, c.data(), static_cast<int>(c.size())) != XRS_OK) c.clear();
+    return c;
+  }
 
  private:
   Queue(xrs_queue* q, size_t size, int d) : q_(q), size_(size), codec_d_(d) {}

@@ -301,6 +301,60 @@ static void TestQueue_Concurrent() {
     FATAL("Update(row=d): got \"%s\"", e.msg.c_str());
 }
 
+// Not in the reference: 32 threads released together (a spin barrier) make
+// one per-stripe Encode and one ReconstOne per round on ONE queue, as many
+// goroutines calling x.Encode per stripe would (xrs_test.go:498-521): the
+// queue must coalesce them (fewer batches than calls, several of 4 stripes or
+// more), and every result equals a second codec's sync call.
+static void TestQueue_Coalesces() {
+  constexpr int kThreads = 32, kRounds = 8, kSize = 4096;
+  auto x = must_new(kData, kParity), y = must_new(kData, kParity);
+  std::unique_ptr<xrs::Queue> q;
+  if (Error e = xrs::Queue::New(*x, kSize, &q, 1024, 50)) FATAL("Queue::New: %s", e.msg.c_str());
+  std::vector<Vects> v(kThreads), ref(kThreads);
+  std::mt19937_64 r(4242);
+  for (int t = 0; t < kThreads; ++t) {
+    v[t] = new_shard_matrix(kData + kParity, kSize);
+    for (int j = 0; j < kData; ++j) fill_random(r, v[t][j]);
+    ref[t] = v[t];
+    if (y->Encode(ref[t])) FATAL("reference encode");
+  }
+  std::atomic<int> arrived{0}, bad{0};
+  auto barrier = [&](int phase) {  // phase p: every thread waits for (p+1) * kThreads arrivals
+    arrived.fetch_add(1);
+    while (arrived.load() < (phase + 1) * kThreads) std::this_thread::yield();
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < kThreads; ++t)
+    th.emplace_back([&, t] {
+      for (int i = 0; i < kRounds; ++i) {
+        barrier(2 * i);
+        for (int j = kData; j < kData + kParity; ++j) std::fill(v[t][j].begin(), v[t][j].end(), 0);
+        if (q->Encode(v[t]) || v[t] != ref[t]) ++bad;
+        const int k = (t + i) % kData;
+        std::fill(v[t][k].begin(), v[t][k].end(), 0x3c);
+        barrier(2 * i + 1);
+        if (q->ReconstOne(v[t], k) || v[t] != ref[t]) ++bad;
+      }
+    });
+  for (auto& t : th) t.join();
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+  const std::vector<uint64_t> sizes = q->BatchSizes();
+  uint64_t batches = 0, stripes = 0, big = 0;
+  for (size_t n = 0; n < sizes.size(); ++n) {
+    batches += sizes[n];
+    stripes += n * sizes[n];
+    if (n >= 4) big += sizes[n];
+  }
+  std::printf("  queue: %d calls in %llu batches (%llu of >= 4 stripes)\n", 2 * kThreads * kRounds,
+              static_cast<unsigned long long>(batches), static_cast<unsigned long long>(big));
+  if (stripes != 2u * kThreads * kRounds) FATAL("stripes run %llu", static_cast<unsigned long long>(stripes));
+  if (batches >= static_cast<uint64_t>(kThreads * kRounds) || big < 3)
+    FATAL("no coalescing: %llu batches for %d calls, %llu of >= 4 stripes",
+          static_cast<unsigned long long>(batches), 2 * kThreads * kRounds,
+          static_cast<unsigned long long>(big));
+}
+
 // Not in the reference: the plain per-stripe calls from 16 threads on ONE
 // codec (a Go server's goroutines sharing an *XRS).  Contended calls batch
 // through the codec's own queue (codec.cpp auto_queue); every result must
@@ -507,6 +561,7 @@ int main(int argc, char** argv) {
       {"TestXRS_Replace", TestXRS_Replace, true},
       {"TestQueue_Concurrent", TestQueue_Concurrent, true},
       {"TestQueue_Oversubscribed", TestQueue_Oversubscribed, true},
+      {"TestQueue_Coalesces", TestQueue_Coalesces, true},
       {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
       {"TestXRS_ReconstPersistent", TestXRS_ReconstPersistent, true},
   };

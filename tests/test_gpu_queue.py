@@ -1,5 +1,6 @@
 """GPU tests of the batching queue (xrs_queue_*): concurrent per-stripe calls
 from many threads, coalesced into device batches, bit-exact to the oracle."""
+import ctypes
 import threading
 
 import numpy as np
@@ -496,10 +497,13 @@ def test_queue_coalesces_barrier_released_callers():
     reference's per-stripe call pattern, xrs_test.go:498-521): the queue
     must run them in fewer batches than calls, several of them holding 4
     stripes or more (xrs_queue_batch_sizes), and every call is bit-exact to
-    the oracle."""
+    the oracle.  The calls go straight to the C ABI with their pointer arrays
+    made beforehand: the Python wrapper's own per-call work, under the GIL,
+    would space 32 threads' calls wider apart than a batch takes to run."""
     size, n_threads, rounds = 4096, 32, 6
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
     q = xrs_amd.XRSQueue(x, size)
+    L, h = xrs_amd.lib(), q.handle
     rng = np.random.Generator(np.random.PCG64(9100))
     work = []
     for t in range(n_threads):
@@ -508,20 +512,21 @@ def test_queue_coalesces_barrier_released_callers():
             v = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
             ref = [a.copy() for a in v]
             o.encode(ref)
-            per.append((v, ref, int(rng.integers(0, D))))
+            arr = (ctypes.c_void_p * (D + P))(*[a.ctypes.data for a in v])
+            per.append((v, ref, int(rng.integers(0, D)), arr))
         work.append(per)
     bar = threading.Barrier(n_threads)
     errors = []
 
     def worker(t):
         try:
-            for r, (v, ref, k) in enumerate(work[t]):
+            for r, (v, ref, k, arr) in enumerate(work[t]):
                 bar.wait(timeout=60)
-                q.encode(v)
+                assert L.xrs_queue_encode(h, arr, D + P) == 0, ("enc rc", t, r)
                 assert all(np.array_equal(a, b) for a, b in zip(v, ref)), ("enc", t, r)
                 v[k][:] = 0x3C
                 bar.wait(timeout=60)
-                q.reconst_one(v, k)
+                assert L.xrs_queue_reconst_one(h, arr, D + P, k) == 0, ("rec rc", t, r)
                 assert np.array_equal(v[k], ref[k]), ("rec", t, r, k)
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))

@@ -17,6 +17,8 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method threa
     "tests/test_gpu_edge.py::test_reconst_batched_persistent_vs_oracle" \
     -s > gpurun_out/r05_first_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r05_first_tests.log; grep "queue:" gpurun_out/r05_first_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 ./tests/cpp/build/xrs_test > gpurun_out/r05_cpp_tests.log 2>&1
+rc=$?; tail -20 gpurun_out/r05_cpp_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05_smoke.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/r05_smoke.log | tail -20; [ $rc -eq 0 ] || exit $rc
 : > gpurun_out/r05_sync_bench.log

@@ -537,6 +537,11 @@ class XRSQueue:
         self.size = size
         self.batch_stripes = _lib.xrs_queue_batch_stripes(h)
 
+    @property
+    def handle(self):
+        """The xrs_queue* (for callers that drive the C ABI directly)."""
+        return self._h
+
     def close(self, _free=_lib.xrs_queue_free):
         """New calls fail from here on; calls in flight complete first."""
         with self._cv:

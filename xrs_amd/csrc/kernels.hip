@@ -852,8 +852,7 @@ void staged_ws_kernel(const StagedArgs<NL, NN, true> a) {
 }
 
 // Wave-specialised 12+4-style Encode (compile-time source count C, P = 4,
-// 16-byte chunks; a ragged half ends in an overlapping chunk, as in the pair
-// kernel, with XRS_ENC_WS_RAGGED=1 for A/B): a block of 2*T lanes works
+// 16-byte chunks, halves a multiple of 16 bytes): a block of 2*T lanes works
 // on T chunks.  Lanes [0, T) load the C data a-halves, form the four parity
 // a-halves and store them, and leave the piggyback terms (data c rides on
 // parity 1 + c % 3, xrs.go:77-100) in LDS; lanes [T, 2T) load the C data
@@ -869,9 +868,7 @@ __global__ __launch_bounds__(2 * T) void enc_ws_kernel(const PairArgs<4, C, true
   const uint64_t gid = logical_block(a.order) * T + t;
   const bool valid = gid < a.total;
   const uint64_t stripe = gid / a.chunks;
-  uint64_t o = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (o > a.last) o = a.last;  // ragged end: overlapping last chunk (both roles alike)
-  const uint64_t off = o + (blane ? a.half : 0);
+  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W) + (blane ? a.half : 0);
   uint32_t acc[P][W];
   if (valid) {
     uint32_t x[C][W];
@@ -1031,13 +1028,18 @@ __global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, 
       v = __builtin_amdgcn_readfirstlane(nexttile[s ^ 1u]);
     }
     // This block takes no more tiles.  The last block to get here resets the
-    // slot: every block's tile atomics are ordered before its arrival (acq_rel
-    // at agent scope), so nothing touches ctr[0] after the reset.
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // slot.  No fence is needed (a release at agent scope writes back the
+    // XCD's L2 on gfx950, +5-11 us per launch measured): lane 0's last tile
+    // atomic has returned (the loop exit reads its value) before its arrival
+    // is issued, so every tile atomic of the launch is performed before the
+    // last arrival; the resets are exchanges whose returned values the busy
+    // store waits for, so they are performed before the host sees the slot
+    // free.
+    if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - 1) {
+      uint32_t r0 = __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t r1 = __hip_atomic_exchange(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" : "+v"(r0), "+v"(r1));  // both returns consumed before the store below
+      __hip_atomic_store(busy, (r0 & r1) & 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }
@@ -2017,8 +2019,10 @@ int launch_pair_t(const PairPlan& p, hipStream_t stream) {
     // it on with 256 chunks per block.
     const char* ew = std::getenv("XRS_ENC_WS");
     const bool ws_on = (ew && *ew) ? ew[0] != '0' : (C <= 12 && p.half <= (128u << 10));
-    const char* rg = std::getenv("XRS_ENC_WS_RAGGED");
-    if (ws_on && (p.half % 16 == 0 || (rg && rg[0] == '1'))) {
+    // (Ragged halves keep the pair kernel: the overlapping-last-chunk form of
+    // this kernel measured 3.3-12% slower at 4,100 / 4,098 / 2,052 / 65,540 B
+    // and +0.8% at 262,146 B, profiles/r05_encws_ragged.log.)
+    if (ws_on && p.half % 16 == 0) {
       int T = 256;  // the block size launched below, which also sets the grid
       if (C == 12 && ew && (std::strcmp(ew, "128") == 0 || std::strcmp(ew, "512") == 0))
         T = std::strcmp(ew, "128") == 0 ? 128 : 512;

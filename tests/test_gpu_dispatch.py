@@ -69,7 +69,8 @@ STAGED = [
     ([15], 1 << 20, "staged_ws_kernel<12, 14, 1, 1, 512, 1>"),
     ([12], 1 << 20, "staged_ws_kernel<12, 15, 1, 1, 512, 1>"),
     ([0, 13], 4096, "staged_ws_kernel<12, 14, 2, 2, 256, 1>"),
-    ([0, 5], 1 << 20, "staged_wsp_kernel<12, 14, 2, 2, 512>"),  # 80 stripes: >= 16 tiles per CU
+    ([0, 5], 1 << 20, "staged_wsp_kernel<12, 14, 2, 2, 512>"),  # 16 stripes: 4 tiles per CU, the gate
+    ([0, 6], 1 << 20, "staged_ws_kernel<12, 14, 2, 2, 512, 1>"),  # 8 stripes: 2 tiles per CU, under it
     ([0, 5, 7], 1 << 20, "staged_ws_kernel<12, 13, 3, 3, 256, 1>"),
 ]
 
@@ -77,7 +78,7 @@ STAGED = [
 @pytest.mark.parametrize("lost,size,kernel", STAGED)
 def test_staged_patterns(codec, lost, size, kernel):
     x, o = codec
-    n = 1024 if size == 4096 else 80 if kernel.startswith("staged_wsp") else 8
+    n = 1024 if size == 4096 else 16 if kernel.startswith("staged_wsp") else 8
     rng = np.random.Generator(np.random.PCG64(12))
     host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)
     o.encode_batch(host, size, n)

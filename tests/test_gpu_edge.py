@@ -245,7 +245,7 @@ def test_reconst_batched_full_grid_vs_oracle(rng, monkeypatch, ct, size, n):
 def test_reconst_batched_persistent_vs_oracle(rng, monkeypatch, wsp, grid, size, n):
     """The persistent wave-specialised kernel (staged_wsp_kernel; XRS_WSP
     forces it for 2-4 lost, the default runs it for 2 lost from 256 to 768
-    KiB halves in launches of at least 16 tiles per CU, test_gpu_dispatch.py): every block takes several tiles from the launch's counter when
+    KiB halves in launches of at least 4 tiles per CU, test_gpu_dispatch.py): every block takes several tiles from the launch's counter when
     XRS_WSP_GRID caps the grid (ragged last tile, uneven tile counts per
     block, both LDS slots reused), every stripe vs the oracle, side effects
     included (xrs.go:236-320)."""
@@ -337,6 +337,9 @@ def test_reconst_persistent_counter_slots_reused(rng, monkeypatch):
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("XRS_WSP", "512")
     monkeypatch.setenv("XRS_WSP_GRID", "8")
+    # a 20-block grid would take the latency-bound all-loads-first kernel;
+    # XRS_STAGED_LATE=1 keeps it on the bandwidth path XRS_WSP forces
+    monkeypatch.setenv("XRS_STAGED_LATE", "1")
     size, n, calls = 4096, 40, 80
     x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
     host = rng.integers(0, 256, size=(n, D + P, size), dtype=np.uint8)

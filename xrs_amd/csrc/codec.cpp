@@ -178,11 +178,20 @@ int run_rows(const std::vector<RowRef>& dst, const std::vector<MulSrc>& msrc,
 // base + s*stripe_stride + i*shard_stride, or, with a per-shard pointer table,
 // at table[i] + s*stripe_stride (shards in separate allocations, or on peer
 // GPUs reached over xGMI).
+//
+// Or, with `ind` (the batching queue's callers' own buffers), every row is
+// indirect (xrs_plan.h kRowInd): stripe s has a table of two device-readable
+// entries per shard, the addresses of its a-half and b-half, at
+// ind + s * ind_stride bytes; row(shard, off) takes off = 0 or S/2.
 struct Layout {
   uint8_t* base;
   size_t shard_stride, stripe_stride;
   const uint64_t* table = nullptr;
+  const uint64_t* ind = nullptr;
+  uint64_t ind_stride = 0;
   RowRef row(int shard, size_t off) const {
+    if (ind)
+      return {reinterpret_cast<uint64_t>(ind + 2 * shard + (off ? 1 : 0)), ind_stride | xrs::kRowInd};
     const uint64_t b = table ? table[shard]
                              : reinterpret_cast<uint64_t>(base) +
                                    static_cast<uint64_t>(shard) * shard_stride;
@@ -971,6 +980,39 @@ int reconst_one_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard
 }
 int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi) {
   return need_vects(x, k, a_need, bi);
+}
+// The queue's batches of callers' own buffers: stripe s's rows through the
+// table at tab + s * tab_stride bytes (two entries per staged row, a- and
+// b-half; Layout::ind).  Rows are numbered as in the queue's staging: Encode,
+// ReconstOne, Reconst the d+p vects; Update [0, p) parity, p old, p+1 new;
+// Replace [0, p) parity, [p, p+n) data.
+int encode_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                 size_t n, void* stream) {
+  return encode_impl(x, {nullptr, 0, 0, nullptr, tab, tab_stride}, size, n,
+                     static_cast<hipStream_t>(stream));
+}
+int reconst_one_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                      size_t n, int k, void* stream) {
+  return reconst_one_impl(x, {nullptr, 0, 0, nullptr, tab, tab_stride}, size, n, k,
+                          static_cast<hipStream_t>(stream));
+}
+int reconst_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size, size_t n,
+                  const int* dp_has, int n_has, const int* need, int n_need, void* stream) {
+  Written w;
+  return reconst_impl(x, {nullptr, 0, 0, nullptr, tab, tab_stride}, size, n, dp_has, n_has, need,
+                      n_need, static_cast<hipStream_t>(stream), &w);
+}
+int update_rows_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                      const int32_t* rows, size_t n, void* stream) {
+  const Layout L{nullptr, 0, 0, nullptr, tab, tab_stride};
+  return update_rows_impl(x, L.row(x->p, 0), L.row(x->p + 1, 0), size, rows, 0, L, n,
+                          static_cast<hipStream_t>(stream));
+}
+int replace_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, const int* rows,
+                  int n_rows, size_t size, size_t n, void* stream) {
+  const Layout P{nullptr, 0, 0, nullptr, tab, tab_stride};
+  const Layout D{nullptr, 0, 0, nullptr, tab + 2 * x->p, tab_stride};
+  return replace_impl(x, D, rows, n_rows, size, P, n, static_cast<hipStream_t>(stream));
 }
 int codec_device(const xrs_codec* x) { return x->device; }
 int codec_d(const xrs_codec* x) { return x->d; }

@@ -130,6 +130,14 @@ __device__ __forceinline__ uint64_t row_addr(const RowRef& r, uint64_t stripe, u
   return r.ptr + stripe * r.stripe_stride + off;
 }
 
+// An indirect row (xrs_plan.h kRowInd): r.ptr is the address of stripe 0's
+// entry in a table of row addresses (device-readable memory, e.g. the queue's
+// pinned row tables), one entry every stripe_stride bytes.
+__device__ __forceinline__ uint64_t row_addr_ind(const RowRef& r, uint64_t stripe, uint64_t off) {
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  return *reinterpret_cast<gu64*>(r.ptr + stripe * (r.stripe_stride & ~kRowInd)) + off;
+}
+
 // ---- XCD-aware block order -------------------------------------------------
 // The dispatcher hands block i to XCD i % 8 (MI355X: 8 XCDs x 32 CUs, one L2
 // each).  Block order maps hardware block b to the logical block it works on:
@@ -244,82 +252,20 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
 // same <4, 12, false, true, 128> shape in the XCD order).
 template <int P, int C, bool ACC, bool VEC, int BS = kBlock, bool PLAIN = false>
 __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
-  constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = (PLAIN ? uint64_t(blockIdx.x) : logical_block(a.order)) * BS + threadIdx.x;
-  if (gid >= a.total) return;
-  const uint64_t stripe = gid / a.chunks;
-  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
-  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
+#define XRS_ROW row_addr
+#include "kbody_pair.h"
+#undef XRS_ROW
+}
 
-  uint32_t acc_a[P][W], acc_b[P][W];
-  if constexpr (ACC) {
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      const uint64_t d = row_addr(a.dst[r], stripe, off);
-      ld<VEC>(acc_a[r], d, nb);
-      ld<VEC>(acc_b[r], d + a.half, nb);
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < P; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc_a[r][w] = acc_b[r][w] = 0u;
-  }
-
-  if constexpr (C != kDyn) {
-    // Compile-time source count: every load issued up front.
-    uint32_t xa[C][W], xb[C][W];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const uint64_t s = row_addr(a.src[c], stripe, off);
-      ld<VEC>(xa[c], s, nb);
-      ld<VEC>(xb[c], s + a.half, nb);
-    }
-#pragma unroll
-    for (int c = 0; c + 1 < C; c += 2)
-      pair_mac2<P, W>(acc_a, acc_b, a.tab[c], a.tab[c + 1], xa[c], xb[c], xa[c + 1], xb[c + 1]);
-    if constexpr (C & 1) pair_mac1<P, W>(acc_a, acc_b, a.tab[C - 1], xa[C - 1], xb[C - 1]);
-    if constexpr (!ACC) {
-      // Piggyback, compile-time XORSet of a (C+P) codec (xrs.go:77-100): data
-      // c rides on parity 1 + c % (P-1).  Compile-time source counts are only
-      // launched for a whole Encode (PairPlan::encode_xs).
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc_b[1 + c % (P - 1)][w] ^= xa[c][w];
-    } else {
-#pragma unroll
-      for (int c = 0; c < C; ++c) piggyback<P, W>(acc_b, a.pbmask, c, xa[c]);
-    }
-  } else {
-    // Runtime source count: groups of kGrp sources, each group's loads issued
-    // together (wave-uniform guards keep the register indexes static).
-    constexpr int kGrp = 6;
-    for (int c0 = 0; c0 < a.n_src; c0 += kGrp) {
-      uint32_t xa[kGrp][W], xb[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (c0 + g < a.n_src) {
-          const uint64_t s = row_addr(a.src[c0 + g], stripe, off);
-          ld<VEC>(xa[g], s, nb);
-          ld<VEC>(xb[g], s + a.half, nb);
-        }
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (c0 + g < a.n_src) {
-          pair_mac1<P, W>(acc_a, acc_b, a.tab[c0 + g], xa[g], xb[g]);
-          piggyback<P, W>(acc_b, a.pbmask, c0 + g, xa[g]);
-        }
-    }
-  }
-
-#pragma unroll
-  for (int r = 0; r < P; ++r) {
-    const uint64_t d = row_addr(a.dst[r], stripe, off);
-    st<VEC>(acc_a[r], d, nb);
-    st<VEC>(acc_b[r], d + a.half, nb);
-  }
+// The pair kernel on indirect rows (the queue's batches of callers' own
+// buffers, xrs_plan.h kRowInd): runtime source count, plain block size.
+template <int P, bool ACC, bool VEC, int C = kDyn>
+__global__ __launch_bounds__(kBlock) void pair_ind_kernel(const PairArgs<P, C, VEC> a) {
+  constexpr int BS = kBlock;
+  constexpr bool PLAIN = false;
+#define XRS_ROW row_addr_ind
+#include "kbody_pair.h"
+#undef XRS_ROW
 }
 
 // ============================================================ rows kernel
@@ -383,82 +329,18 @@ __device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, c
 
 template <int R, int NM, int NX, bool ACC, bool VEC, int BS = kBlock>
 __global__ __launch_bounds__(BS) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
-  constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = logical_block(a.order) * BS + threadIdx.x;
-  if (gid >= a.total) return;
-  const uint64_t stripe = gid / a.chunks;
-  uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
-  const int nb = VEC ? 16 : static_cast<int>(a.len - off < 4 ? a.len - off : 4);
+#define XRS_ROW row_addr
+#include "kbody_rows.h"
+#undef XRS_ROW
+}
 
-  uint32_t acc[R][W];
-  if constexpr (ACC) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) ld<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-  }
-
-  if constexpr (NM != kDyn && NX != kDyn) {
-    uint32_t xm[NM > 0 ? NM : 1][W], xx[NX > 0 ? NX : 1][W];
-    // Raised priority while this wave issues its loads, so fresh waves get
-    // their requests out ahead of waves that are computing (measured +1.7%
-    // on ReconstOne 1 MiB; tools/kbench.hip "rw prio").
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < NM; ++m) ld<VEC>(xm[m], row_addr(a.msrc[m], stripe, off), nb);
-#pragma unroll
-    for (int x = 0; x < NX; ++x) ld<VEC>(xx[x], row_addr(a.xsrc[x], stripe, off), nb);
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int m = 0; m + 1 < NM; m += 2) rows_mac2<R, W>(acc, a.tab[m], a.tab[m + 1], xm[m], xm[m + 1]);
-    if constexpr (NM & 1) rows_mac1<R, W>(acc, a.tab[NM - 1], xm[NM - 1]);
-#pragma unroll
-    for (int x = 0; x < NX; ++x) rows_xor<R, W>(acc, a.xmask[x], xx[x]);
-  } else if (a.grouped) {
-    // Runtime counts, small grid (latency-bound): groups of kGrp rows, each
-    // group's loads issued together, so a launch pays ceil(rows / kGrp)
-    // memory round trips instead of one per row.
-    constexpr int kGrp = 8;
-    for (int m0 = 0; m0 < a.nm; m0 += kGrp) {
-      uint32_t v[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (m0 + g < a.nm) ld<VEC>(v[g], row_addr(a.msrc[m0 + g], stripe, off), nb);
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (m0 + g < a.nm) rows_mac1<R, W>(acc, a.tab[m0 + g], v[g]);
-    }
-    for (int x0 = 0; x0 < a.nx; x0 += kGrp) {
-      uint32_t v[kGrp][W];
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (x0 + g < a.nx) ld<VEC>(v[g], row_addr(a.xsrc[x0 + g], stripe, off), nb);
-#pragma unroll
-      for (int g = 0; g < kGrp; ++g)
-        if (x0 + g < a.nx) rows_xor<R, W>(acc, a.xmask[x0 + g], v[g]);
-    }
-  } else {
-    // Runtime counts, large grid: one row at a time (measured: grouping 8
-    // loads per wave cost 0-2% at 4 KiB and 2-7% at 1 MiB over seven (d, p)
-    // in the XCD order; profiles/r01_others_rows_grouped{0,1}.log).
-    for (int m = 0; m < a.nm; ++m) {
-      uint32_t v[W];
-      ld<VEC>(v, row_addr(a.msrc[m], stripe, off), nb);
-      rows_mac1<R, W>(acc, a.tab[m], v);
-    }
-    for (int x = 0; x < a.nx; ++x) {
-      uint32_t v[W];
-      ld<VEC>(v, row_addr(a.xsrc[x], stripe, off), nb);
-      rows_xor<R, W>(acc, a.xmask[x], v);
-    }
-  }
-
-#pragma unroll
-  for (int r = 0; r < R; ++r) st<VEC>(acc[r], row_addr(a.dst[r], stripe, off), nb);
+// The rows kernel on indirect rows (xrs_plan.h kRowInd): runtime counts.
+template <int R, bool ACC, bool VEC, int NM = kDyn, int NX = kDyn>
+__global__ __launch_bounds__(kBlock) void rows_ind_kernel(const RowsArgs<R, NM, NX, VEC> a) {
+  constexpr int BS = kBlock;
+#define XRS_ROW row_addr_ind
+#include "kbody_rows.h"
+#undef XRS_ROW
 }
 
 // ============================================================ staged kernel
@@ -1246,82 +1128,17 @@ struct UpdRowsArgs {
 
 template <int P, bool VEC>
 __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P, VEC> a) {
-  constexpr int W = VEC ? 4 : 1;
-  const uint64_t gid = logical_block(a.order) * kBlock + threadIdx.x;
-  if (gid >= a.total) return;
-  const uint64_t stripe = gid / a.chunks;
-  const uint64_t off = a.off0 + (gid - stripe * a.chunks) * (4 * W);
-  const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
-  // rows == nullptr: one row for the whole batch (plain Update), table 0.
-  const int r = a.rows ? a.rows[stripe] - a.row0 : 0;
-  if (r < 0 || r >= a.nrows) return;  // another launch's row, or not a data row
-
-  uint32_t oa[W], ob[W], na[W], nw[W], pa[P][W], pb[P][W];
-  const uint64_t o = row_addr(a.old_row, stripe, off), n = row_addr(a.new_row, stripe, off);
-  ld<VEC>(oa, o, nb);
-  ld<VEC>(ob, o + a.half, nb);
-  ld<VEC>(na, n, nb);
-  ld<VEC>(nw, n + a.half, nb);
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const uint64_t dq = row_addr(a.dst[q], stripe, off);
-    ld<VEC>(pa[q], dq, nb);
-    ld<VEC>(pb[q], dq + a.half, nb);
-  }
-  const int pbq = a.pbq[r];
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const uint32_t da = oa[w] ^ na[w], db = ob[w] ^ nw[w];
-    const Sel sa = sel_of(da), sb = sel_of(db);
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const GfTab t = a.tab[r][q];
-      pa[q][w] ^= gmul(t, sa);
-      pb[q][w] = xor_masked(pb[q][w] ^ gmul(t, sb), da, pbq == q ? ~0u : 0u);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const uint64_t dq = row_addr(a.dst[q], stripe, off);
-    st<VEC>(pa[q], dq, nb);
-    st<VEC>(pb[q], dq + a.half, nb);
-  }
+#define XRS_ROW row_addr
+#include "kbody_update.h"
+#undef XRS_ROW
 }
 
-// ============================================================ copy kernel
-// The batching queue's gather / scatter (xrs_plan.h CopyPlan): block (x, y, z)
-// moves chunks [256x, 256x + 256) of 16 bytes of piece y of stripe z between
-// the caller's row (its address from the stripe's row table, in registered
-// host memory read over PCIe) and the compact device staging.  A piece of 16
-// bytes or more ends in one overlapping 16-byte chunk (the copy is pure, so
-// the overlap rewrites equal bytes); a shorter one is copied byte by byte.
-// Any alignment: MI355X runs unaligned dwordx4 accesses (kernels above).
-constexpr int kCopyBlock = 256;
-
-struct CopyArgs {
-  CopyPiece piece[kMaxPieces];
-  const uint64_t* tab;
-  uint64_t nrows;
-  uint64_t stage, stripe_bytes, row_bytes;
-  uint32_t gather;
-};
-
-__global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CopyArgs a) {
-  const CopyPiece pc = a.piece[blockIdx.y];
-  const uint64_t stripe = blockIdx.z;
-  const uint64_t c = (static_cast<uint64_t>(blockIdx.x) * kCopyBlock + threadIdx.x) * 16;
-  if (c >= pc.len) return;
-  const uint64_t row = a.tab[stripe * a.nrows + pc.row] + pc.off;
-  const uint64_t stg = a.stage + stripe * a.stripe_bytes + pc.row * a.row_bytes + pc.off;
-  const uint64_t src = a.gather ? row : stg, dst = a.gather ? stg : row;
-  if (pc.len >= 16) {
-    const uint64_t o = c + 16 > pc.len ? pc.len - 16 : c;
-    *reinterpret_cast<gu32x4*>(dst + o) = *reinterpret_cast<const gu32x4*>(src + o);
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i)
-      if (i < pc.len) reinterpret_cast<gu8*>(dst)[i] = reinterpret_cast<const gu8*>(src)[i];
-  }
+// update_rows on indirect rows (xrs_plan.h kRowInd).
+template <int P, bool VEC>
+__global__ __launch_bounds__(kBlock) void update_rows_ind_kernel(const UpdRowsArgs<P, VEC> a) {
+#define XRS_ROW row_addr_ind
+#include "kbody_update.h"
+#undef XRS_ROW
 }
 
 }  // namespace
@@ -1793,18 +1610,19 @@ int launch_staged_t(const StagedPlan& p, hipStream_t stream) {
       // vects +2.9 / -0.1 / +4.2 / +2.6%; 2 / 4 / 8 MiB -1.8 / +0.7 / -14.7%,
       // so larger halves keep the one-shot kernel; 3 lost -2..-4% and
       // 256-chunk tiles -5..-21%, profiles/r04_wsp_sizes.log).
-      // Only launches of at least XRS_WSP_MIN_TILES (per CU, default 16:
-      // 64 stripes of 1 MiB): the round-4 per-launch counter (stream-ordered
-      // alloc + memset + free) cost 2-7 us per synchronous call, which smaller
-      // launches did not win back (tools/wsp_call_overhead.py,
-      // profiles/r04_wsp_overhead.log: 4 / 16 / 64 / 256 stripes of 1 MiB
-      // +7.0 / +2.4 / -4.5 / -34 us); the counter is now a self-resetting
-      // slot (tile_counters).  XRS_WSP=0 turns it off, =512 / =256 forces it
-      // (A/B, tests).
+      // Only launches of at least XRS_WSP_MIN_TILES tiles per CU (default
+      // 4: 16 stripes of 1 MiB).  With the self-resetting counter slots
+      // (tile_counters) a synchronous call costs what the kernel does:
+      // 1 / 4 / 16 / 64 / 256 stripes of 1 MiB (0.25 .. 64 tiles per CU)
+      // -0.1 / +0.6 / -3.3 / -7.7 / -37 us against the one-shot kernel
+      // (tools/wsp_call_overhead.py, profiles/r05_wsp_overhead.log; the
+      // round-4 per-launch alloc + memset + free cost +7.0 / +2.4 us at 4 /
+      // 16 stripes, r04_wsp_overhead.log, hence a gate of 16 tiles then).
+      // XRS_WSP=0 turns it off, =512 / =256 forces it (A/B, tests).
       const char* pv = std::getenv("XRS_WSP");
       const bool wsp_off = pv && pv[0] == '0';
       const char* mt = std::getenv("XRS_WSP_MIN_TILES");
-      const uint64_t min_tiles = (mt && *mt) ? std::strtoull(mt, nullptr, 10) : uint64_t(16);
+      const uint64_t min_tiles = (mt && *mt) ? std::strtoull(mt, nullptr, 10) : uint64_t(4);
       int wsp = kNotLaunched;
       if (pv && std::strcmp(pv, "256") == 0) wsp = launch_staged_wsp<NL, NN, 256>(a, p, stream);
       else if (pv && std::strcmp(pv, "512") == 0) wsp = launch_staged_wsp<NL, NN, 512>(a, p, stream);
@@ -1886,7 +1704,7 @@ int launch_staged_r(const StagedPlan& p, hipStream_t s) {
   return launch_staged_t<4, 4, VEC>(p, s);
 }
 
-template <int P, bool VEC>
+template <int P, bool VEC, bool IND = false>
 int launch_update_rows_t(const UpdRowsPlan& p, hipStream_t stream) {
   UpdRowsArgs<P, VEC> a;
   std::memset(&a, 0, sizeof(a));
@@ -1909,18 +1727,22 @@ int launch_update_rows_t(const UpdRowsPlan& p, hipStream_t stream) {
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kPair, VEC, p.half, blocks);
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
-  XRS_LAUNCH((update_rows_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kBlock), stream, a);
+  if constexpr (IND)
+    XRS_LAUNCH((update_rows_ind_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+               stream, a);
+  else
+    XRS_LAUNCH((update_rows_kernel<P, VEC>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), stream, a);
   return static_cast<int>(hipGetLastError());
 }
 
-template <bool VEC>
+template <bool VEC, bool IND = false>
 int launch_update_rows_p(const UpdRowsPlan& p, hipStream_t s) {
   switch (p.P) {
-    case 1: return launch_update_rows_t<1, VEC>(p, s);
-    case 2: return launch_update_rows_t<2, VEC>(p, s);
-    case 3: return launch_update_rows_t<3, VEC>(p, s);
-    case 4: return launch_update_rows_t<4, VEC>(p, s);
+    case 1: return launch_update_rows_t<1, VEC, IND>(p, s);
+    case 2: return launch_update_rows_t<2, VEC, IND>(p, s);
+    case 3: return launch_update_rows_t<3, VEC, IND>(p, s);
+    case 4: return launch_update_rows_t<4, VEC, IND>(p, s);
     default: return static_cast<int>(hipErrorInvalidValue);
   }
 }
@@ -1965,6 +1787,61 @@ void fill_rows_args(RowsArgs<R, NM, NX, VEC>& a, const RowsPlan& p) {
   a.chunks = VEC ? (p.end - p.off0 + 15) / 16 : (p.end - p.off0 + 3) / 4;
   a.last = (VEC && p.overlap) ? p.end - 16 : ~uint64_t(0);
   a.total = a.chunks * p.n_stripes;
+}
+
+// Indirect-row launches (xrs_plan.h kRowInd: the queue's batches of callers'
+// own buffers): runtime counts, 256-thread blocks, the family's block order.
+// Small batches of host-resident rows are bound by PCIe round trips, not by
+// the kernel's shape.
+template <int P, bool ACC, bool VEC>
+int launch_pair_ind_t(const PairPlan& p, hipStream_t stream) {
+  PairArgs<P, kDyn, VEC> a;
+  fill_pair_args(a, p);
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kPair, VEC, p.half, blocks);
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  XRS_LAUNCH((pair_ind_kernel<P, ACC, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+             stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <bool ACC, bool VEC>
+int launch_pair_ind_p(const PairPlan& p, hipStream_t s) {
+  switch (p.P) {
+    case 1: return launch_pair_ind_t<1, ACC, VEC>(p, s);
+    case 2: return launch_pair_ind_t<2, ACC, VEC>(p, s);
+    case 3: return launch_pair_ind_t<3, ACC, VEC>(p, s);
+    case 4: return launch_pair_ind_t<4, ACC, VEC>(p, s);
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+}
+
+template <int R, bool ACC, bool VEC>
+int launch_rows_ind_t(const RowsPlan& p, hipStream_t stream) {
+  RowsArgs<R, kDyn, kDyn, VEC> a;
+  fill_rows_args(a, p);
+  if (a.total == 0) return 0;
+  const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
+  a.order = block_order(Shape::kRows, VEC, p.len, blocks);
+  a.grouped = blocks < kLatencyGrid;  // as launch_rows_t: grouped loads on small grids
+  (void)hipGetLastError();  // report this launch's error, not an earlier call's
+  XRS_LAUNCH((rows_ind_kernel<R, ACC, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+             stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <bool ACC, bool VEC>
+int launch_rows_ind_r(const RowsPlan& p, hipStream_t s) {
+  switch (p.R) {
+    case 1: return launch_rows_ind_t<1, ACC, VEC>(p, s);
+    case 2: return launch_rows_ind_t<2, ACC, VEC>(p, s);
+    case 3: return launch_rows_ind_t<3, ACC, VEC>(p, s);
+    case 4: return launch_rows_ind_t<4, ACC, VEC>(p, s);
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
 }
 
 template <int P, int C, bool ACC, bool VEC>
@@ -2310,6 +2187,7 @@ int split_launch(Plan p, uint64_t len, bool aligned, F launch, bool overlap_ok =
 }
 
 bool row_aligned(const RowRef& r) { return aligned16(r.ptr) && aligned16(r.stripe_stride); }
+bool row_ind(const RowRef& r) { return (r.stripe_stride & kRowInd) != 0; }
 
 // Two rows of `len` bytes share a byte in some pair of stripes s, t <
 // n_stripes (row a of stripe s against row b of stripe t), or step
@@ -2390,6 +2268,21 @@ size_t traced_kernels(char* buf, size_t cap) {
 int launch_pair(const PairPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.P < 1 || p0.P > kMaxOut || p0.C < 0 || p0.C > kMaxSrc) return static_cast<int>(hipErrorInvalidValue);
+  bool ind = false;
+  for (int c = 0; c < p0.C; ++c) ind = ind || row_ind(p0.src[c]);
+  for (int r = 0; r < p0.P; ++r) ind = ind || row_ind(p0.dst[r]);
+  if (ind) {  // every row indirect; ragged end as a byte-granular second launch
+    for (int c = 0; c < p0.C; ++c)
+      if (!row_ind(p0.src[c])) return static_cast<int>(hipErrorInvalidValue);
+    for (int r = 0; r < p0.P; ++r)
+      if (!row_ind(p0.dst[r])) return static_cast<int>(hipErrorInvalidValue);
+    PairPlan pp = p0;
+    pp.overlap = false;
+    return split_launch(pp, p0.half, false, [s](const PairPlan& p, bool vec) {
+      if (p.acc) return vec ? launch_pair_ind_p<true, true>(p, s) : launch_pair_ind_p<true, false>(p, s);
+      return vec ? launch_pair_ind_p<false, true>(p, s) : launch_pair_ind_p<false, false>(p, s);
+    });
+  }
   bool al = true;
   for (int c = 0; c < p0.C; ++c) al = al && row_aligned(p0.src[c]);
   for (int r = 0; r < p0.P; ++r) al = al && row_aligned(p0.dst[r]);
@@ -2410,6 +2303,8 @@ bool tile_counters(int dev) { return ctr_ring(dev) != nullptr; }
 
 int launch_staged(const StagedPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int m = 0; m < p0.na; ++m)  // indirect rows: the step plan (rows kernels) runs them
+    if (row_ind(p0.asrc[m])) return kStagedDecline;
   if (p0.nd < 1 || p0.nd > p0.na || p0.nd > p0.nb || p0.na > kStSrc || p0.nb > kStB || p0.nl < 0 ||
       p0.nl > kStOut || p0.nn < 0 || p0.nn > kStOut)
     return static_cast<int>(hipErrorInvalidValue);
@@ -2440,6 +2335,16 @@ int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.P < 1 || p0.P > kMaxOut || p0.nrows < 1 || p0.nrows > kMaxSrc || (!p0.rows && p0.nrows != 1))
     return static_cast<int>(hipErrorInvalidValue);
+  bool ind = row_ind(p0.old_row) || row_ind(p0.new_row);
+  for (int q = 0; q < p0.P; ++q) ind = ind || row_ind(p0.dst[q]);
+  if (ind) {  // every row indirect (the queue's callers' buffers)
+    bool all = row_ind(p0.old_row) && row_ind(p0.new_row);
+    for (int q = 0; q < p0.P; ++q) all = all && row_ind(p0.dst[q]);
+    if (!all) return static_cast<int>(hipErrorInvalidValue);
+    return split_launch(p0, p0.half, false, [s](const UpdRowsPlan& p, bool vec) {
+      return vec ? launch_update_rows_p<true, true>(p, s) : launch_update_rows_p<false, true>(p, s);
+    });
+  }
   bool al = row_aligned(p0.old_row) && row_aligned(p0.new_row);
   for (int q = 0; q < p0.P; ++q) al = al && row_aligned(p0.dst[q]);
   return split_launch(p0, p0.half, al, [s](const UpdRowsPlan& p, bool vec) {
@@ -2447,37 +2352,6 @@ int launch_update_rows(const UpdRowsPlan& p0, void* stream) {
   });
 }
 
-int launch_copy(const CopyPlan& p, void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.npieces > static_cast<uint32_t>(kMaxPieces) || !p.tab || !p.stage) return static_cast<int>(hipErrorInvalidValue);
-  if (p.npieces == 0 || p.n_stripes == 0) return 0;
-  CopyArgs a;
-  std::memset(&a, 0, sizeof(a));
-  uint64_t maxlen = 0;
-  for (uint32_t i = 0; i < p.npieces; ++i) {
-    if (p.piece[i].row >= p.nrows) return static_cast<int>(hipErrorInvalidValue);
-    a.piece[i] = p.piece[i];
-    maxlen = std::max<uint64_t>(maxlen, p.piece[i].len);
-  }
-  a.nrows = p.nrows;
-  a.stripe_bytes = p.stripe_bytes;
-  a.row_bytes = p.row_bytes;
-  a.gather = p.gather ? 1u : 0u;
-  const uint64_t xb = (maxlen + 16 * kCopyBlock - 1) / (16 * kCopyBlock);
-  if (xb == 0 || xb > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
-  (void)hipGetLastError();  // report this launch's error, not an earlier call's
-  constexpr uint64_t kMaxZ = 65535;  // grid z limit: stripes in chunks
-  for (uint64_t s0 = 0; s0 < p.n_stripes; s0 += kMaxZ) {
-    const uint64_t nz = std::min(kMaxZ, p.n_stripes - s0);
-    a.tab = reinterpret_cast<const uint64_t*>(p.tab) + s0 * p.nrows;
-    a.stage = p.stage + s0 * p.stripe_bytes;
-    XRS_LAUNCH(copy_kernel, dim3(static_cast<unsigned>(xb), p.npieces, static_cast<unsigned>(nz)),
-               dim3(kCopyBlock), s, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return static_cast<int>(e);
-  }
-  return 0;
-}
 #endif  // XRS_HAS_PART(3)
 
 #if XRS_HAS_PART(4)
@@ -2485,6 +2359,20 @@ int launch_rows(const RowsPlan& p0, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p0.R < 1 || p0.R > kMaxOut || p0.NM < 0 || p0.NM > kMaxSrc || p0.NX < 0 || p0.NX > kMaxXor)
     return static_cast<int>(hipErrorInvalidValue);
+  bool ind = false, all = true;
+  auto note = [&](const RowRef& r) { (row_ind(r) ? ind : all) = row_ind(r); };
+  for (int m = 0; m < p0.NM; ++m) note(p0.msrc[m]);
+  for (int x = 0; x < p0.NX; ++x) note(p0.xsrc[x]);
+  for (int r = 0; r < p0.R; ++r) note(p0.dst[r]);
+  if (ind) {  // every row indirect (the queue's callers' buffers)
+    if (!all) return static_cast<int>(hipErrorInvalidValue);
+    RowsPlan rp = p0;
+    rp.overlap = false;
+    return split_launch(rp, p0.len, false, [s](const RowsPlan& p, bool vec) {
+      if (p.acc) return vec ? launch_rows_ind_r<true, true>(p, s) : launch_rows_ind_r<true, false>(p, s);
+      return vec ? launch_rows_ind_r<false, true>(p, s) : launch_rows_ind_r<false, false>(p, s);
+    });
+  }
   bool al = true;
   for (int m = 0; m < p0.NM; ++m) al = al && row_aligned(p0.msrc[m]);
   for (int x = 0; x < p0.NX; ++x) al = al && row_aligned(p0.xsrc[x]);

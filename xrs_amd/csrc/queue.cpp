@@ -58,7 +58,6 @@
 
 #include "hostreg.h"
 #include "xrs_hip.h"
-#include "xrs_plan.h"
 
 namespace xrs_detail {
 int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
@@ -66,6 +65,17 @@ int encode_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stri
 int reconst_one_dev(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
                     size_t stripe_stride, size_t n_stripes, int k, void* stream);
 int need_set(const xrs_codec* x, int k, std::vector<int>* a_need, int* bi);
+// table mode: the callers' rows through per-stripe row tables (codec.cpp)
+int encode_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                 size_t n, void* stream);
+int reconst_one_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                      size_t n, int k, void* stream);
+int reconst_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size, size_t n,
+                  const int* dp_has, int n_has, const int* need, int n_need, void* stream);
+int update_rows_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, size_t size,
+                      const int32_t* rows, size_t n, void* stream);
+int replace_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, const int* rows,
+                  int n_rows, size_t size, size_t n, void* stream);
 int codec_device(const xrs_codec* x);
 int codec_d(const xrs_codec* x);
 int codec_p(const xrs_codec* x);
@@ -120,13 +130,13 @@ struct Batch {
   uint8_t* dev = nullptr;
   int32_t* rows = nullptr;      // pinned, mapped: Update's data row per slot
   int32_t* rows_dev = nullptr;  // its device address (read by the kernel)
-  // Row tables (pinned, mapped; nrows per slot): the device address of each
-  // staged row's bytes -- the caller's own vect when it lies in registered
-  // memory (hostreg.h), else the slot's row in `host`.  A batch with any
-  // registered slot runs gather kernel -> op on `dev` -> scatter kernel.
+  // Row tables (pinned, mapped; per slot, two entries per staged row: the
+  // device addresses of its a-half and b-half) -- the caller's own vect when
+  // it lies in registered memory (hostreg.h), else the slot's row in `host`.
+  // A batch with any registered slot runs its kernels through the tables, in
+  // place on the callers' buffers over PCIe (indirect rows, xrs_plan.h).
   uint64_t* tab = nullptr;
   uint64_t* tab_dev = nullptr;
-  std::vector<xrs::CopyPiece> pin, pout;  // the batch's pieces (one layout per key)
   hipStream_t stream = nullptr;
   volatile uint32_t* flag = nullptr;  // pinned host word the stream writes `launches` to
   uint32_t* flag_dev = nullptr;
@@ -227,60 +237,57 @@ int xrs_queue::launch(Batch& bt) {
                             : upd || rec || rep ? 0 : static_cast<size_t>(bt.key - 1) * size;
   const size_t dn_len = enc || upd || rep ? static_cast<size_t>(p) * size
                                           : rec ? static_cast<size_t>(d + p) * size : size;
-  // Registered callers: gather their rows into device staging, run, scatter
-  // the outputs back, all on the GPU (XRS_QUEUE_REG=0: never).
+  // Registered callers: the kernels read and write the callers' own buffers
+  // (and unregistered slots' pinned staging) through the row tables, in
+  // place over PCIe, one launch as in zero-copy mode (XRS_QUEUE_REG=0: never).
   const bool table = reg_ok && bt.n_reg.load(std::memory_order_acquire) > 0;
   const bool zc = !table && bt.host_dev && n * stripe_bytes <= zc_max;
   uint8_t* base = (zc ? bt.host_dev : bt.dev) + bo;
   uint8_t *hst = bt.host + bo, *dst = bt.dev + bo;
-  auto copy = [&](const std::vector<xrs::CopyPiece>& pcs, bool gather) {
-    xrs::CopyPlan cp;
-    std::memset(&cp, 0, sizeof(cp));
-    cp.tab = reinterpret_cast<uint64_t>(bt.tab_dev);
-    cp.nrows = static_cast<uint32_t>(nrows);
-    cp.stage = reinterpret_cast<uint64_t>(dst);
-    cp.stripe_bytes = stripe_bytes;
-    cp.row_bytes = size;
-    cp.n_stripes = n;
-    cp.gather = gather;
-    for (size_t i0 = 0; i0 < pcs.size(); i0 += xrs::kMaxPieces) {
-      cp.npieces = static_cast<uint32_t>(std::min<size_t>(xrs::kMaxPieces, pcs.size() - i0));
-      for (uint32_t i = 0; i < cp.npieces; ++i) cp.piece[i] = pcs[i0 + i];
-      if (xrs::launch_copy(cp, bt.stream) != 0) return XRS_ERR_HIP;
-    }
-    return XRS_OK;
-  };
   int e = 0;
-  if (table)
-    e = copy(bt.pin, true);
-  else if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
-                                   n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
-    e = XRS_ERR_HIP;
-  if (!e) {
+  if (table) {
+    const size_t ts = 2 * nrows * sizeof(uint64_t);
     if (enc)
-      e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
+      e = xrs_detail::encode_table(codec, bt.tab_dev, ts, size, n, bt.stream);
     else if (rep)
-      e = xrs_replace_batched(codec, base + static_cast<size_t>(p) * size, size, stripe_bytes,
-                              bt.pat_has.data(), static_cast<int>(bt.pat_has.size()), size, base,
-                              size, stripe_bytes, n, bt.stream);
+      e = xrs_detail::replace_table(codec, bt.tab_dev, ts, bt.pat_has.data(),
+                                    static_cast<int>(bt.pat_has.size()), size, n, bt.stream);
     else if (rec)
-      e = xrs_reconst_batched(codec, base, size, size, stripe_bytes, n, bt.pat_has.data(),
-                              static_cast<int>(bt.pat_has.size()), bt.pat_need.data(),
-                              static_cast<int>(bt.pat_need.size()), bt.stream);
-    else if (upd)  // one launch for every row: each stripe carries its own
-      e = xrs_update_rows_batched(codec, base + static_cast<size_t>(p) * size, stripe_bytes,
-                                  base + static_cast<size_t>(p + 1) * size, stripe_bytes, size,
-                                  bt.rows_dev, base, size, stripe_bytes, n, bt.stream);
+      e = xrs_detail::reconst_table(codec, bt.tab_dev, ts, size, n, bt.pat_has.data(),
+                                    static_cast<int>(bt.pat_has.size()), bt.pat_need.data(),
+                                    static_cast<int>(bt.pat_need.size()), bt.stream);
+    else if (upd)
+      e = xrs_detail::update_rows_table(codec, bt.tab_dev, ts, size, bt.rows_dev, n, bt.stream);
     else
-      e = xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n, bt.key - 1,
-                                      bt.stream);
+      e = xrs_detail::reconst_one_table(codec, bt.tab_dev, ts, size, n, bt.key - 1, bt.stream);
+  } else {
+    if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
+                                n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
+      e = XRS_ERR_HIP;
+    if (!e) {
+      if (enc)
+        e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
+      else if (rep)
+        e = xrs_replace_batched(codec, base + static_cast<size_t>(p) * size, size, stripe_bytes,
+                                bt.pat_has.data(), static_cast<int>(bt.pat_has.size()), size, base,
+                                size, stripe_bytes, n, bt.stream);
+      else if (rec)
+        e = xrs_reconst_batched(codec, base, size, size, stripe_bytes, n, bt.pat_has.data(),
+                                static_cast<int>(bt.pat_has.size()), bt.pat_need.data(),
+                                static_cast<int>(bt.pat_need.size()), bt.stream);
+      else if (upd)  // one launch for every row: each stripe carries its own
+        e = xrs_update_rows_batched(codec, base + static_cast<size_t>(p) * size, stripe_bytes,
+                                    base + static_cast<size_t>(p + 1) * size, stripe_bytes, size,
+                                    bt.rows_dev, base, size, stripe_bytes, n, bt.stream);
+      else
+        e = xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n, bt.key - 1,
+                                        bt.stream);
+    }
+    if (!e && !zc &&
+        hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
+                         hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
+      e = XRS_ERR_HIP;
   }
-  if (!e && table)
-    e = copy(bt.pout, false);
-  else if (!e && !zc &&
-           hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
-                            hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
-    e = XRS_ERR_HIP;
   if (!e && hipStreamWriteValue32(bt.stream, bt.flag_dev, ++bt.launches, 0) != hipSuccess)
     e = XRS_ERR_HIP;
   if (e) (void)hipStreamSynchronize(bt.stream);  // nothing of it may still run
@@ -468,14 +475,6 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       nb.released.store(0, std::memory_order_relaxed);
       nb.err = 0;
       nb.n_reg.store(0, std::memory_order_relaxed);
-      nb.pin.clear();
-      nb.pout.clear();
-      for (const Piece& pc : in)
-        nb.pin.push_back({static_cast<uint32_t>(pc.row), static_cast<uint32_t>(pc.off),
-                          static_cast<uint32_t>(pc.len)});
-      for (const Piece& pc : out)
-        nb.pout.push_back({static_cast<uint32_t>(pc.row), static_cast<uint32_t>(pc.off),
-                           static_cast<uint32_t>(pc.len)});
       nb.opened = Clock::now();
       if (has) {
         nb.pat_has = *has;
@@ -492,12 +491,15 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   Batch& bt = *bp;
   uint8_t* st = bt.host + bo + slot * stripe_bytes;
   if (row >= 0) bt.rows[slot] = row;
-  if (reg_ok) {
-    uint64_t* tb = bt.tab + slot * nrows;
+  if (reg_ok) {  // the slot's row table: a- and b-half of every row it uses
+    uint64_t* tb = bt.tab + slot * 2 * nrows;
     const uint64_t sd = reinterpret_cast<uint64_t>(bt.host_dev + bo + slot * stripe_bytes);
     for (const auto* ps : {&in, &out})
-      for (const Piece& pc : *ps)
-        tb[pc.row] = reg ? regdev[pc.row] : sd + static_cast<uint64_t>(pc.row) * size;
+      for (const Piece& pc : *ps) {
+        const uint64_t a = reg ? regdev[pc.row] : sd + static_cast<uint64_t>(pc.row) * size;
+        tb[2 * pc.row] = a;
+        tb[2 * pc.row + 1] = a + size / 2;
+      }
     if (reg) bt.n_reg.fetch_add(1, std::memory_order_relaxed);
   }
   if (!reg)
@@ -596,7 +598,7 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
     bt.rows_dev = static_cast<int32_t*>(dp);
     // row tables for registered callers (at most 16 MiB per batch, else the
     // queue copies every call through `host`; XRS_QUEUE_REG=0: always)
-    const size_t tb = q->max_batch * q->nrows * sizeof(uint64_t);
+    const size_t tb = q->max_batch * 2 * q->nrows * sizeof(uint64_t);
     if (q->reg_ok && tb <= (16u << 20) &&
         hipHostMalloc(reinterpret_cast<void**>(&bt.tab), tb, hipHostMallocMapped) == hipSuccess &&
         hipHostGetDevicePointer(&dp, bt.tab, 0) == hipSuccess && bt.host_dev) {

@@ -37,6 +37,11 @@ struct RowRef {
   uint64_t ptr;            // device address of this row in stripe 0
   uint64_t stripe_stride;  // bytes between consecutive stripes
 };
+// An indirect row (stripe_stride has this bit): ptr is the device-readable
+// address of stripe 0's entry in a table of row addresses, and stripe s's row
+// starts at the address stored at ptr + s * (stripe_stride & ~kRowInd).  The
+// batching queue addresses its callers' own (registered) buffers this way.
+constexpr uint64_t kRowInd = uint64_t(1) << 63;
 
 constexpr int kMaxOut = 4;   // outputs per launch (parity rows / rebuilt rows)
 constexpr int kMaxSrc = 24;  // GF sources per launch (more: chained ACC launches)
@@ -127,27 +132,6 @@ struct UpdRowsPlan {
   bool overlap;        // unused (accumulates: the ragged end is its own launch)
 };
 
-// "copy" kernel: the batching queue's gather / scatter between the callers'
-// own buffers (registered host memory, reached over PCIe) and a compact device
-// staging batch.  Stripe s has a table of nrows row addresses (the caller's
-// vects: tab[s * nrows + row]); each piece moves bytes [off, off + len) of one
-// row between that address and stage + s * stripe_bytes + row * row_bytes.
-constexpr int kMaxPieces = 64;  // pieces per launch (more: several launches)
-struct CopyPiece {
-  uint32_t row, off, len;
-};
-struct CopyPlan {
-  uint64_t tab;   // device-readable address of n_stripes * nrows row addresses
-  uint32_t nrows;
-  uint32_t npieces;
-  CopyPiece piece[kMaxPieces];
-  uint64_t stage;         // device address of stripe 0, row 0 of the staging batch
-  uint64_t stripe_bytes;  // staging bytes per stripe
-  uint64_t row_bytes;     // staging bytes per row
-  uint64_t n_stripes;
-  bool gather;  // true: table rows -> staging; false: staging -> table rows
-};
-
 // Kernel launchers (kernels.hip).  Return a hipError_t value as int.
 int launch_pair(const PairPlan& plan, void* stream);
 int launch_rows(const RowsPlan& plan, void* stream);
@@ -157,7 +141,6 @@ int launch_rows(const RowsPlan& plan, void* stream);
 constexpr int kStagedDecline = -1;
 int launch_staged(const StagedPlan& plan, void* stream);
 int launch_update_rows(const UpdRowsPlan& plan, void* stream);
-int launch_copy(const CopyPlan& plan, void* stream);
 // Launch trace (diagnostics): record every kernel instantiation launched from
 // here on (on: clears the record); traced_kernels writes "name count" lines.
 void trace_kernels(bool on);

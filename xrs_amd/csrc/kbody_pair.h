@@ -1,6 +1,7 @@
 // kbody_pair.h -- the pair kernel's body (kernels.hip), included inside the
-// kernel functions with XRS_ROW(row, stripe, off) naming the row addressing:
-// row_addr for pair_kernel, row_addr_ind for pair_ind_kernel.  Not a header.
+// kernel functions: XRS_IND 0 with XRS_ROW(row, stripe, off) naming the row
+// addressing (pair_kernel), XRS_IND 1 for table rows (pair_ind_kernel, runtime
+// source count only).  Not a header.
   constexpr int W = VEC ? 4 : 1;
   const uint64_t gid = (PLAIN ? uint64_t(blockIdx.x) : logical_block(a.order)) * BS + threadIdx.x;
   if (gid >= a.total) return;
@@ -9,11 +10,27 @@
   if (VEC && off > a.last) off = a.last;  // ragged end: overlapping last chunk
   const int nb = VEC ? 16 : static_cast<int>(a.half - off < 4 ? a.half - off : 4);
 
+#if XRS_IND
+  // Table rows: every row's base address read up front, in one round trip.
+  // vmcnt retires in order, so a table read issued after a row's data loads
+  // would also wait for them: one round trip per row (measured 2x per batch).
+  uint64_t db[P], sb[kMaxSrc];
+#pragma unroll
+  for (int r = 0; r < P; ++r) db[r] = row_base_ind(a.dst[r], stripe);
+#pragma unroll
+  for (int c = 0; c < kMaxSrc; ++c)
+    if (c < a.n_src) sb[c] = row_base_ind(a.src[c], stripe);
+#define XRS_DST(r) (db[r] + off)
+#define XRS_SRC(c) (sb[c] + off)
+#else
+#define XRS_DST(r) XRS_ROW(a.dst[r], stripe, off)
+#define XRS_SRC(c) XRS_ROW(a.src[c], stripe, off)
+#endif
   uint32_t acc_a[P][W], acc_b[P][W];
   if constexpr (ACC) {
 #pragma unroll
     for (int r = 0; r < P; ++r) {
-      const uint64_t d = XRS_ROW(a.dst[r], stripe, off);
+      const uint64_t d = XRS_DST(r);
       ld<VEC>(acc_a[r], d, nb);
       ld<VEC>(acc_b[r], d + a.half, nb);
     }
@@ -29,7 +46,7 @@
     uint32_t xa[C][W], xb[C][W];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const uint64_t s = XRS_ROW(a.src[c], stripe, off);
+      const uint64_t s = XRS_SRC(c);
       ld<VEC>(xa[c], s, nb);
       ld<VEC>(xb[c], s + a.half, nb);
     }
@@ -53,12 +70,18 @@
     // Runtime source count: groups of kGrp sources, each group's loads issued
     // together (wave-uniform guards keep the register indexes static).
     constexpr int kGrp = 6;
+#if XRS_IND
+#pragma unroll
+    for (int c0 = 0; c0 < kMaxSrc; c0 += kGrp) {  // unrolled: sb[] indexes static
+      if (c0 >= a.n_src) break;
+#else
     for (int c0 = 0; c0 < a.n_src; c0 += kGrp) {
+#endif
       uint32_t xa[kGrp][W], xb[kGrp][W];
 #pragma unroll
       for (int g = 0; g < kGrp; ++g)
         if (c0 + g < a.n_src) {
-          const uint64_t s = XRS_ROW(a.src[c0 + g], stripe, off);
+          const uint64_t s = XRS_SRC(c0 + g);
           ld<VEC>(xa[g], s, nb);
           ld<VEC>(xb[g], s + a.half, nb);
         }
@@ -73,7 +96,9 @@
 
 #pragma unroll
   for (int r = 0; r < P; ++r) {
-    const uint64_t d = XRS_ROW(a.dst[r], stripe, off);
+    const uint64_t d = XRS_DST(r);
     st<VEC>(acc_a[r], d, nb);
     st<VEC>(acc_b[r], d + a.half, nb);
   }
+#undef XRS_DST
+#undef XRS_SRC

@@ -133,9 +133,9 @@ __device__ __forceinline__ uint64_t row_addr(const RowRef& r, uint64_t stripe, u
 // An indirect row (xrs_plan.h kRowInd): r.ptr is the address of stripe 0's
 // entry in a table of row addresses (device-readable memory, e.g. the queue's
 // pinned row tables), one entry every stripe_stride bytes.
-__device__ __forceinline__ uint64_t row_addr_ind(const RowRef& r, uint64_t stripe, uint64_t off) {
+__device__ __forceinline__ uint64_t row_base_ind(const RowRef& r, uint64_t stripe) {
   typedef __attribute__((address_space(1))) const uint64_t gu64;
-  return *reinterpret_cast<gu64*>(r.ptr + stripe * (r.stripe_stride & ~kRowInd)) + off;
+  return *reinterpret_cast<gu64*>(r.ptr + stripe * (r.stripe_stride & ~kRowInd));
 }
 
 // ---- XCD-aware block order -------------------------------------------------
@@ -252,9 +252,11 @@ __device__ __forceinline__ void piggyback(uint32_t (&acc_b)[P][W], const uint32_
 // same <4, 12, false, true, 128> shape in the XCD order).
 template <int P, int C, bool ACC, bool VEC, int BS = kBlock, bool PLAIN = false>
 __global__ __launch_bounds__(BS) void pair_kernel(const PairArgs<P, C, VEC> a) {
+#define XRS_IND 0
 #define XRS_ROW row_addr
 #include "kbody_pair.h"
 #undef XRS_ROW
+#undef XRS_IND
 }
 
 // The pair kernel on indirect rows (the queue's batches of callers' own
@@ -263,9 +265,9 @@ template <int P, bool ACC, bool VEC, int C = kDyn>
 __global__ __launch_bounds__(kBlock) void pair_ind_kernel(const PairArgs<P, C, VEC> a) {
   constexpr int BS = kBlock;
   constexpr bool PLAIN = false;
-#define XRS_ROW row_addr_ind
+#define XRS_IND 1
 #include "kbody_pair.h"
-#undef XRS_ROW
+#undef XRS_IND
 }
 
 // ============================================================ rows kernel
@@ -329,18 +331,20 @@ __device__ __forceinline__ void rows_xor(uint32_t (&acc)[R][W], uint32_t mask, c
 
 template <int R, int NM, int NX, bool ACC, bool VEC, int BS = kBlock>
 __global__ __launch_bounds__(BS) void rows_kernel(const RowsArgs<R, NM, NX, VEC> a) {
+#define XRS_IND 0
 #define XRS_ROW row_addr
 #include "kbody_rows.h"
 #undef XRS_ROW
+#undef XRS_IND
 }
 
 // The rows kernel on indirect rows (xrs_plan.h kRowInd): runtime counts.
 template <int R, bool ACC, bool VEC, int NM = kDyn, int NX = kDyn>
 __global__ __launch_bounds__(kBlock) void rows_ind_kernel(const RowsArgs<R, NM, NX, VEC> a) {
   constexpr int BS = kBlock;
-#define XRS_ROW row_addr_ind
+#define XRS_IND 1
 #include "kbody_rows.h"
-#undef XRS_ROW
+#undef XRS_IND
 }
 
 // ============================================================ staged kernel
@@ -1128,17 +1132,19 @@ struct UpdRowsArgs {
 
 template <int P, bool VEC>
 __global__ __launch_bounds__(kBlock) void update_rows_kernel(const UpdRowsArgs<P, VEC> a) {
+#define XRS_IND 0
 #define XRS_ROW row_addr
 #include "kbody_update.h"
 #undef XRS_ROW
+#undef XRS_IND
 }
 
 // update_rows on indirect rows (xrs_plan.h kRowInd).
 template <int P, bool VEC>
 __global__ __launch_bounds__(kBlock) void update_rows_ind_kernel(const UpdRowsArgs<P, VEC> a) {
-#define XRS_ROW row_addr_ind
+#define XRS_IND 1
 #include "kbody_update.h"
-#undef XRS_ROW
+#undef XRS_IND
 }
 
 }  // namespace

@@ -253,8 +253,10 @@ def oracle_encode_batch(o, host):
 # 1 MiB and 1 MiB + 2: the 12+4 Encode from 512 KiB halves runs the
 # plain-order kernel specialization (pair_kernel<4, 12, false, true, 128, true>);
 # aligned halves up to 128 KiB the wave-specialised enc_ws_kernel<12, 256>
-# (XRS_ENC_WS=0: the pair kernel there too; =128 / 512: other block sizes).
-@pytest.mark.parametrize("enc_ws", ["", "0", "128", "512"])
+# (XRS_ENC_WS=0: the pair kernel there too; =128 / 512: other block sizes;
+# any other value, e.g. 1 or "on", forces it on at 256 chunks per block,
+# 1 MiB included).
+@pytest.mark.parametrize("enc_ws", ["", "0", "128", "512", "1", "on"])
 @pytest.mark.parametrize("size", [4096, 2, 1026, 4112, 4128, 65536, 262144, 1 << 20, (1 << 20) + 2])
 def test_encode_batched_vs_oracle(cuda, rng, monkeypatch, size, enc_ws):
     if enc_ws:

@@ -8,6 +8,7 @@ update_rows_ind_kernel) over the queue's per-batch row address table
 Every result, side effects included, is compared with the oracle
 (oracle/xrs_oracle.c, following xrs.go:103-387)."""
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -19,9 +20,6 @@ from oracle.oracle_c import OracleXRS
 pytestmark = pytest.mark.gpu
 
 
-def _ind_launches(tr):
-    """Launches of the indirect-row kernels in a traced_kernels() dict."""
-    return sum(n for k, n in tr.items() if "_ind_kernel" in k)
 D, P = 12, 4
 PAGE = 4096
 
@@ -60,6 +58,11 @@ class Arena:
             L.xrs_host_free(self.ptr)
         else:
             assert L.xrs_host_unregister(self.ptr) == 0
+
+
+def _ind_launches(tr):
+    """Launches of the indirect-row kernels in a traced_kernels() dict."""
+    return sum(n for k, n in tr.items() if "_ind_kernel" in k)
 
 
 def _fill(rng, arrs):
@@ -314,3 +317,81 @@ def test_shared_codec_registered_concurrent():
     assert not errors, errors[:3]
     tr = xrs_amd.traced_kernels()
     assert tr.get("host:sync_in_place", 0) + _ind_launches(tr) > 0, tr
+
+
+FUZZ_CODECS = [(12, 4), (10, 4), (6, 3), (4, 2), (5, 5), (20, 4), (1, 2), (30, 6), (3, 9), (16, 8)]
+FUZZ_OPS = ["encode", "reconst_one", "reconst", "update", "replace"]
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("XRS_FUZZ_SEEDS", "4"))))
+@pytest.mark.parametrize("via", ["sync", "queue"])
+def test_registered_fuzz_vs_oracle(seed, via):
+    """Random codecs, sizes, per-vect skews and operations on registered
+    vects, through the in-place sync calls or a queue (table mode: the
+    indirect-row kernels, chained launches past 24 sources included), against
+    the oracle applied to copies; every vect is compared, side effects
+    included."""
+    rng = np.random.Generator(np.random.PCG64(7700 + seed + (0 if via == "sync" else 50000)))
+    xrs_amd.trace_kernels(True)
+    try:
+        for case in range(12):
+            d, p = FUZZ_CODECS[int(rng.integers(0, len(FUZZ_CODECS)))]
+            size = int(rng.choice([2, 34, 4096, 4112, 65538]))
+            x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
+            ar = Arena((2 * d + p + 2) * (size + 32), "alloc")
+            q = xrs_amd.XRSQueue(x, size) if via == "queue" else None
+            api = q if q is not None else x
+            try:
+                def take(count):
+                    out = [ar.take(size, int(rng.integers(0, 16))) for _ in range(count)]
+                    _fill(rng, out)
+                    return out
+
+                a = take(d + p)
+                o.encode(a)
+                b = [t.copy() for t in a]
+                op = FUZZ_OPS[int(rng.integers(0, len(FUZZ_OPS)))]
+                tag = (seed, case, d, p, size, op, via)
+                if op == "encode":
+                    for t in a[d:]:
+                        t[:] = 0x33
+                    api.encode(a)
+                elif op == "reconst_one":
+                    k = int(rng.integers(0, d))
+                    a[k][:] = 0
+                    api.reconst_one(a, k)
+                elif op == "reconst":
+                    lost = [int(t) for t in rng.permutation(d + p)[: int(rng.integers(1, p + 1))]]
+                    need = lost[: int(rng.integers(1, len(lost) + 1))]
+                    has = [i for i in range(d + p) if i not in lost]
+                    for i in lost:
+                        a[i][:] = 0xA5
+                        b[i][:] = 0xA5
+                    api.reconst(a, has, need)
+                    o.reconst(b, has, need)
+                elif op == "update":
+                    row = int(rng.integers(0, d))
+                    new = take(1)[0]
+                    api.update(a[row], new, row, a[d:])
+                    o.update(b[row], new, row, b[d:])
+                else:
+                    k = int(rng.integers(1, d + 1))
+                    rows = [int(t) for t in rng.permutation(d)[:k]]
+                    data = take(k)
+                    api.replace(data, rows, a[d:])
+                    o.replace(data, rows, b[d:])
+                for j, (s_, t_) in enumerate(zip(a, b)):
+                    if not np.array_equal(s_, t_):
+                        bad = np.nonzero(s_ != t_)[0]
+                        raise AssertionError(f"{tag}: vect {j}: {len(bad)} bytes differ, first at {bad[0]}")
+            finally:
+                if q is not None:
+                    q.close()
+                ar.close()
+    finally:
+        xrs_amd.trace_kernels(False)
+    tr = xrs_amd.traced_kernels()
+    if via == "queue":
+        assert _ind_launches(tr) > 0, tr
+    else:
+        assert tr.get("host:sync_in_place", 0) > 0, tr

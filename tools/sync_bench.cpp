@@ -138,9 +138,12 @@ int main(int argc, char** argv) {
   // queue calls (Encode, ReconstOne, Update, Reconst of one loss pattern,
   // Replace of one rows set) on queues of two vect sizes, and the plain API
   // on the shared codec (auto queue) at three sizes; queues are created and
-  // freed under load every second.  Results are not checked here (the GPU
-  // tests do that); any error or a call stuck 20 s is a failure (exit 5 / 6,
-  // with the queue dump).
+  // freed under load every second.  Even threads' vects are registered
+  // (xrs_host_alloc: in-place sync calls, table-mode queue batches); thread 1
+  // unregisters and re-registers its own buffer every 64 calls, so the
+  // registry changes under the other callers' lookups.  Results are not
+  // checked here (the GPU tests do that); any error or a call stuck 20 s is a
+  // failure (exit 5 / 6, with the queue dump).
   if (argc > 1 && std::strcmp(argv[1], "stress") == 0) {
     const int secs = argc > 2 ? std::atoi(argv[2]) : 60;
     const int threads = argc > 3 ? std::atoi(argv[3]) : 32;
@@ -162,12 +165,35 @@ int main(int argc, char** argv) {
       th.emplace_back([&, t] {
         uint64_t r = 0x9E3779B97F4A7C15ull * (t + 1);
         auto rnd = [&] { r ^= r << 13; r ^= r >> 7; r ^= r << 17; return r; };
-        std::vector<std::vector<uint8_t>> v(16, std::vector<uint8_t>(65536, (uint8_t)t));
+        constexpr size_t kVect = 65536;
+        std::vector<std::vector<uint8_t>> v;
+        std::vector<uint8_t> churn;
+        uint8_t* reg = nullptr;
         std::vector<uint8_t*> p;
-        for (auto& x : v) p.push_back(x.data());
+        if (t % 2 == 0 && (reg = static_cast<uint8_t*>(xrs_host_alloc(16 * kVect)))) {
+          for (int j = 0; j < 16; ++j) p.push_back(reg + j * kVect);
+        } else if (t == 1) {
+          churn.assign(16 * kVect, static_cast<uint8_t>(t));
+          for (int j = 0; j < 16; ++j) p.push_back(churn.data() + j * kVect);
+        } else {
+          v.assign(16, std::vector<uint8_t>(kVect, static_cast<uint8_t>(t)));
+          for (auto& x : v) p.push_back(x.data());
+        }
+        bool churn_reg = false;
+        long mine = 0;
         const int has[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 14, 15}, need[] = {0, 13};
         const int rows[] = {3, 7};
         while (!stop.load(std::memory_order_relaxed)) {
+          if (t == 1 && mine++ % 64 == 0) {  // flip the registration (no call in flight)
+            const int e = churn_reg ? xrs_host_unregister(churn.data())
+                                    : xrs_host_register(churn.data(), churn.size());
+            if (e) {
+              std::printf("STRESS FAIL: host (un)register rc %d\n", e);
+              std::fflush(stdout);
+              std::_Exit(5);
+            }
+            churn_reg = !churn_reg;
+          }
           const int op = static_cast<int>(rnd() % 10);
           int rc = 0;
           if (op < 5) {  // explicit queue
@@ -198,6 +224,8 @@ int main(int argc, char** argv) {
           }
           ++calls;
         }
+        if (churn_reg) (void)xrs_host_unregister(churn.data());
+        if (reg) xrs_host_free(reg);
       });
     // every second: replace one explicit queue (xrs_queue_free under load),
     // and watch for progress

@@ -20,6 +20,17 @@ def test_cpp_host_logic():
     assert "PASS" in r.stdout
 
 
+@pytest.mark.parametrize("san", ["tsan", "asan"])
+def test_hostreg_table_under_sanitizers(san):
+    """The registered-range table (xrs_amd/csrc/hostreg.cpp) alone: lookups,
+    readers racing register / unregister, retired tables freed."""
+    build()
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", f"hostreg_test_{san}")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS hostreg" in r.stdout
+
+
 @pytest.mark.gpu
 def test_cpp_all_on_gpu():
     if not os.path.exists(BIN):

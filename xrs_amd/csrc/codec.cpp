@@ -1437,9 +1437,10 @@ bool reg_vects(uint8_t* const* v, int n, const std::vector<int>& use, size_t siz
   }();
   if (off) return false;
   dev->assign(n, 0);
+  const xrs_detail::HostRangesView ranges;
   for (int i : use) {
     if (i < 0 || i >= n || !v[i]) return false;
-    const uint64_t a = xrs_detail::host_ranges_device(v[i], size);
+    const uint64_t a = ranges.device(v[i], size);
     if (!a) return false;
     (*dev)[i] = a;
   }

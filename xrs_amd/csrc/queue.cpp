@@ -437,13 +437,16 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
   // in registered host memory (hostreg.h): then no copy on this thread.
   uint64_t regdev[xrs_queue::kMaxRows];
   bool reg = reg_ok;
-  for (const auto* ps : {&in, &out})
-    for (const Piece& pc : *ps)
-      if (reg) {
-        const uint64_t a = xrs_detail::host_ranges_device(pc.host, size);
-        reg = a != 0 && pc.row >= 0 && static_cast<size_t>(pc.row) < nrows;
-        if (reg) regdev[pc.row] = a;
-      }
+  if (reg) {
+    const xrs_detail::HostRangesView ranges;
+    for (const auto* ps : {&in, &out})
+      for (const Piece& pc : *ps)
+        if (reg) {
+          const uint64_t a = ranges.device(pc.host, size);
+          reg = a != 0 && pc.row >= 0 && static_cast<size_t>(pc.row) < nrows;
+          if (reg) regdev[pc.row] = a;
+        }
+  }
   Batch* bp;
   size_t slot;
   uint32_t seq;

@@ -1798,7 +1798,8 @@ void fill_rows_args(RowsArgs<R, NM, NX, VEC>& a, const RowsPlan& p) {
 // Indirect-row launches (xrs_plan.h kRowInd: the queue's batches of callers'
 // own buffers): runtime counts, 256-thread blocks, the family's block order.
 // Small batches of host-resident rows are bound by PCIe round trips, not by
-// the kernel's shape.
+// the kernel's shape, so the bodies read every row base first (one round
+// trip) and group their data loads (kbody_*.h, XRS_IND).
 template <int P, bool ACC, bool VEC>
 int launch_pair_ind_t(const PairPlan& p, hipStream_t stream) {
   PairArgs<P, kDyn, VEC> a;
@@ -1832,7 +1833,7 @@ int launch_rows_ind_t(const RowsPlan& p, hipStream_t stream) {
   const uint64_t blocks = (a.total + kBlock - 1) / kBlock;
   if (blocks > kMaxBlocks) return static_cast<int>(hipErrorInvalidConfiguration);
   a.order = block_order(Shape::kRows, VEC, p.len, blocks);
-  a.grouped = blocks < kLatencyGrid;  // as launch_rows_t: grouped loads on small grids
+  a.grouped = true;  // (the indirect body always runs the grouped loop)
   (void)hipGetLastError();  // report this launch's error, not an earlier call's
   XRS_LAUNCH((rows_ind_kernel<R, ACC, VEC>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
              stream, a);

@@ -68,10 +68,8 @@
     }
   } else {
     // Runtime source count: groups of kGrp sources, each group's loads issued
-    // together (wave-uniform guards keep the register indexes static).  Table
-    // rows (host memory, one PCIe round trip per group): 12, a 12+4 Encode in
-    // one group.
-    constexpr int kGrp = XRS_IND ? 12 : 6;
+    // together (wave-uniform guards keep the register indexes static).
+    constexpr int kGrp = 6;
 #if XRS_IND
 #pragma unroll
     for (int c0 = 0; c0 < kMaxSrc; c0 += kGrp) {  // unrolled: sb[] indexes static

@@ -61,21 +61,20 @@
     // Runtime counts, small grid (latency-bound): groups of kGrp rows, each
     // group's loads issued together, so a launch pays ceil(rows / kGrp)
     // memory round trips instead of one per row.
-    constexpr int kGrp = 8, kGrpM = XRS_IND ? 12 : kGrp;  // table rows: 12+4 ReconstOne's
-                                                             // 12 products in one group
+    constexpr int kGrp = 8;
 #if XRS_IND
 #pragma unroll
-    for (int m0 = 0; m0 < kMaxSrc; m0 += kGrpM) {  // unrolled: mb[] indexes static
+    for (int m0 = 0; m0 < kMaxSrc; m0 += kGrp) {  // unrolled: mb[] indexes static
       if (m0 >= a.nm) break;
 #else
-    for (int m0 = 0; m0 < a.nm; m0 += kGrpM) {
+    for (int m0 = 0; m0 < a.nm; m0 += kGrp) {
 #endif
-      uint32_t v[kGrpM][W];
+      uint32_t v[kGrp][W];
 #pragma unroll
-      for (int g = 0; g < kGrpM; ++g)
+      for (int g = 0; g < kGrp; ++g)
         if (m0 + g < a.nm) ld<VEC>(v[g], XRS_MSRC(m0 + g), nb);
 #pragma unroll
-      for (int g = 0; g < kGrpM; ++g)
+      for (int g = 0; g < kGrp; ++g)
         if (m0 + g < a.nm) rows_mac1<R, W>(acc, a.tab[m0 + g], v[g]);
     }
 #if XRS_IND

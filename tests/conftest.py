@@ -33,3 +33,20 @@ def golden_codecs():
 def rng():
     # Fixed seeds (the reference seeds from the clock, xrs_test.go:26-31).
     return np.random.Generator(np.random.PCG64(0x5EED))
+
+
+@pytest.fixture(autouse=True)
+def _device_clean_after_gpu_test(request):
+    """After every GPU test, collect garbage (codecs and queues freed here, not
+    inside the next test) and synchronize the device, so an asynchronous
+    fault fails the test that caused it rather than a later one."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    import gc
+
+    gc.collect()
+    torch.cuda.synchronize()

@@ -38,6 +38,9 @@ class Arena:
             assert self.ptr
             self.buf = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
         else:
+            # whole pages (HIP pins pages), all inside this buffer, so no page
+            # another object shares is pinned with it
+            nbytes = (nbytes + PAGE - 1) // PAGE * PAGE
             raw = np.empty(nbytes + PAGE, np.uint8)
             off = (-raw.ctypes.data) % PAGE
             self.raw = raw

@@ -802,8 +802,8 @@ def per_stripe_queue(args):
                   "cpu_note": ("cpu_cores = process CPU time (callers' copies + the queue's "
                                "launcher and completion threads) / wall time")}
     # the same callers with their vects in registered memory (xrs_host_alloc:
-    # the cgo shim's pinned buffer pool): no CPU copy through staging, the
-    # queue's gather / scatter kernels move the rows (queue.cpp table mode)
+    # the cgo shim's pinned buffer pool): no CPU copy through staging, one
+    # indirect-row launch per batch in place (queue.cpp table mode)
     lines, err = child("queuereg")
     out["registered"] = err or {"by_callers": {str(x["threads"]): {k: x[k] for k in (
         "gibps", "stripes_per_s", "stripes_per_batch", "run_us_per_batch", "wait_us_per_batch",

@@ -520,6 +520,103 @@ static void TestXRS_ReconstPersistent() {
 
 // A vect shorter or longer than vects[0] is rejected before the C ABI call
 // (which reads and writes `size` bytes of every vect): ADVICE r1.
+// Not in the reference: per-stripe calls on registered host memory
+// (xrs_host_alloc, and xrs_host_register on one thread's buffer).  8 threads
+// on ONE codec and ONE queue: lone sync calls run in place, contended ones go
+// through the codec's auto-queue, queue calls batch in table mode (one
+// indirect-row launch over the callers' bytes).  Every result equals the same
+// call on plain copies.  Vects start 2 bytes past a 16-byte boundary.
+static void TestRegistered_SyncAndQueue() {
+  constexpr size_t S = 4096, kStride = S + 64;
+  constexpr int kRows = kData + kParity + 4;  // + new data, two Replace rows, spare
+  auto x = must_new(kData, kParity);
+  xrs_queue* q = nullptr;
+  if (xrs_queue_new(x->codec(), S, 64, 50, &q)) FATAL("xrs_queue_new");
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      const size_t bytes = (kRows * kStride + 65535) / 65536 * 65536;
+      uint8_t* base = nullptr;
+      std::vector<uint8_t> own;
+      if (t == 3) {  // caller memory pinned with xrs_host_register
+        own.resize(bytes + 65536);
+        base = own.data() + (65536 - reinterpret_cast<uintptr_t>(own.data()) % 65536) % 65536;
+        if (xrs_host_register(base, bytes)) {
+          ++bad;
+          return;
+        }
+      } else if (!(base = static_cast<uint8_t*>(xrs_host_alloc(bytes)))) {
+        ++bad;
+        return;
+      }
+      std::vector<uint8_t*> v(kRows);
+      for (int j = 0; j < kRows; ++j) v[j] = base + j * kStride + 2;
+      std::mt19937_64 r(700 + t);
+      auto fill = [&](uint8_t* p) { for (size_t i = 0; i < S; ++i) p[i] = static_cast<uint8_t>(r()); };
+      auto copy = [&](int from, int to) {
+        Vects c = new_shard_matrix(to - from, S);
+        for (int j = from; j < to; ++j) std::memcpy(c[j - from].data(), v[j], S);
+        return c;
+      };
+      auto same = [&](const Vects& c, int from) {
+        for (size_t j = 0; j < c.size(); ++j)
+          if (std::memcmp(c[j].data(), v[from + j], S)) return false;
+        return true;
+      };
+      const int n = kData + kParity;
+      for (int it = 0; it < 24; ++it) {
+        const bool viaq = (it + t) % 2 == 0;
+        for (int j = 0; j < kData; ++j) fill(v[j]);
+        Vects ref = copy(0, n);
+        int rc = viaq ? xrs_queue_encode(q, v.data(), n) : xrs_encode(x->codec(), v.data(), n, S);
+        if (rc || x->Encode(ref) || !same(ref, 0)) ++bad;
+        const int k = static_cast<int>(r() % kData);
+        std::memset(v[k], 0, S);
+        rc = viaq ? xrs_queue_reconst_one(q, v.data(), n, k) : xrs_reconst_one(x->codec(), v.data(), n, S, k);
+        if (rc || !same(ref, 0)) ++bad;
+        // Update of row k with fresh bytes (v[n] holds them)
+        fill(v[n]);
+        Vects newd = copy(n, n + 1);
+        rc = viaq ? xrs_queue_update(q, v[k], v[n], k, v.data() + kData, kParity)
+                  : xrs_update(x->codec(), v[k], v[n], S, k, v.data() + kData, kParity);
+        auto pr = xrs::slices(ref, kData);
+        if (rc || x->Update(ref[k], newd[0], k, pr)) ++bad;
+        std::memcpy(v[k], v[n], S);
+        ref[k] = newd[0];
+        if (!same(ref, 0)) ++bad;
+        // Replace of two rows (v[n+1], v[n+2] hold their data)
+        const std::vector<int> rows = {k, (k + 7) % kData};
+        fill(v[n + 1]);
+        fill(v[n + 2]);
+        Vects rd = copy(n + 1, n + 3);
+        rc = viaq ? xrs_queue_replace(q, v.data() + n + 1, rows.data(), 2, v.data() + kData, kParity)
+                  : xrs_replace(x->codec(), v.data() + n + 1, rows.data(), 2, S, v.data() + kData, kParity);
+        if (rc || x->Replace(xrs::slices(rd), rows, xrs::slices(ref, kData)) || !same(ref, 0)) ++bad;
+        // Reconst of one data and one parity vect, both needed
+        const std::vector<int> lost = {k, kData + 1 + it % (kParity - 1)};
+        std::vector<int> has;
+        for (int j = 0; j < n; ++j)
+          if (!is_in(j, lost)) has.push_back(j);
+        for (int j : lost) {
+          std::memset(v[j], 0x5a, S);
+          std::fill(ref[j].begin(), ref[j].end(), 0x5a);
+        }
+        rc = viaq ? xrs_queue_reconst(q, v.data(), n, has.data(), 14, lost.data(), 2)
+                  : xrs_reconst(x->codec(), v.data(), n, S, has.data(), 14, lost.data(), 2);
+        if (rc || x->Reconst(ref, has, lost) || !same(ref, 0)) ++bad;
+      }
+      if (t == 3) {
+        if (xrs_host_unregister(base)) ++bad;
+      } else {
+        xrs_host_free(base);
+      }
+    });
+  for (auto& t : th) t.join();
+  xrs_queue_free(q);
+  if (bad) FATAL("%d mismatches or errors", bad.load());
+}
+
 static void TestMismatchedVects() {
   std::unique_ptr<XRS> x;
   if (Error e = XRS::New(kData, kParity, &x)) FATAL("New: %s", e.msg.c_str());
@@ -565,6 +662,7 @@ int main(int argc, char** argv) {
       {"TestQueue_Coalesces", TestQueue_Coalesces, true},
       {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
       {"TestXRS_ReconstPersistent", TestXRS_ReconstPersistent, true},
+      {"TestRegistered_SyncAndQueue", TestRegistered_SyncAndQueue, true},
   };
   for (const T& t : tests) {
     if (cpu_only && t.gpu) continue;

@@ -50,3 +50,7 @@ def _device_clean_after_gpu_test(request):
 
     gc.collect()
     torch.cuda.synchronize()
+    if os.environ.get("XRS_TEST_H2D_PROBE") == "1":  # diagnostics: a pageable copy up and back
+        h = np.arange(1 << 20, dtype=np.uint32).view(np.uint8)
+        assert np.array_equal(torch.from_numpy(h).cuda().cpu().numpy(), h)
+        torch.cuda.synchronize()

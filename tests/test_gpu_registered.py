@@ -48,12 +48,26 @@ class Arena:
             self.ptr = self.buf.ctypes.data
             assert L.xrs_host_register(self.ptr, nbytes) == 0
         self.pos = 0
+        self.taken = []
 
     def take(self, n, skew=0):
         start = (self.pos + 15) // 16 * 16 + skew
         assert start + n <= len(self.buf), "arena too small"
         self.pos = start + n
+        self.taken.append((start, start + n))
         return self.buf[start:start + n]
+
+    def canary(self, byte=0xC5):
+        """Fill the whole arena (before any take) with `byte`."""
+        self.buf[:] = byte
+        self.canary_byte = byte
+
+    def untouched(self):
+        """Offsets outside every taken vect whose canary byte changed."""
+        mask = np.ones(len(self.buf), bool)
+        for a, b in self.taken:
+            mask[a:b] = False
+        return np.nonzero(mask & (self.buf != self.canary_byte))[0]
 
     def close(self):
         L = xrs_amd.lib()
@@ -342,6 +356,7 @@ def test_registered_fuzz_vs_oracle(seed, via):
             size = int(rng.choice([2, 34, 4096, 4112, 65538]))
             x, o = xrs_amd.XRS(d, p), OracleXRS(d, p)
             ar = Arena((2 * d + p + 2) * (size + 32), "alloc")
+            ar.canary()  # nothing outside the vects may be written
             q = xrs_amd.XRSQueue(x, size) if via == "queue" else None
             api = q if q is not None else x
             try:
@@ -387,6 +402,9 @@ def test_registered_fuzz_vs_oracle(seed, via):
                     if not np.array_equal(s_, t_):
                         bad = np.nonzero(s_ != t_)[0]
                         raise AssertionError(f"{tag}: vect {j}: {len(bad)} bytes differ, first at {bad[0]}")
+                stray = ar.untouched()
+                assert len(stray) == 0, f"{tag}: {len(stray)} bytes outside the vects written, first at {stray[0]} " \
+                    f"(vects at {ar.taken})"
             finally:
                 if q is not None:
                     q.close()

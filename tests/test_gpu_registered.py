@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 D, P = 12, 4
 PAGE = 4096
+_RETIRED = []  # unregistered arenas, kept alive (Arena.close)
 
 
 class Arena:
@@ -75,6 +76,9 @@ class Arena:
             L.xrs_host_free(self.ptr)
         else:
             assert L.xrs_host_unregister(self.ptr) == 0
+            # keep the pages for the session: later buffers (and the runtime's
+            # pageable copies from them) do not land on just-unpinned pages
+            _RETIRED.append(self.raw)
 
 
 def _ind_launches(tr):

@@ -781,8 +781,8 @@ def per_stripe_queue(args):
     exe = os.path.join(ROOT, "tools", "sync_bench")
     if not os.path.exists(exe):
         return {"skipped": "tools/sync_bench not built (build() makes it)"}
-    def child(mode):
-        cmd = [exe, "4096", mode] + (["50"] if mode.startswith("queue") else []) + [
+    def child(mode, size=4096):
+        cmd = [exe, str(size), mode] + (["50"] if mode.startswith("queue") else []) + [
             str(t) for t in args.queue_callers]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
@@ -817,6 +817,15 @@ def per_stripe_queue(args):
             for x in lines}
     out["plain_api"] = plain("syncmt")
     out["plain_api_registered"] = plain("syncmtreg")
+    # 64 KiB vects (1 MiB per stripe), where the callers' copies dominate the
+    # CPU cost: the queue with plain and with registered vects
+    big = {}
+    for name, mode in (("plain", "queue"), ("registered", "queuereg")):
+        lines, err = child(mode, 65536)
+        big[name] = err or {str(x["threads"]): {k: x[k] for k in (
+            "gibps", "stripes_per_batch", "run_us_per_batch", "cpu_cores", "cpu_seconds_per_gib")
+            if k in x} for x in lines}
+    out["queue_64k"] = big
     return out
 
 

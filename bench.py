@@ -509,6 +509,19 @@ def headline(R: Rank, args):
     return launches, step_bytes, rank_seconds, kernels, (enc_shard, rec_shard), samples
 
 
+def config5_plan(requested: int, fits: int, rank: int, world: int, gather=None) -> dict:
+    """Config 5's split (no GPU call): every rank runs the same count -- the
+    requested one per rank, or what the emptiest GPU's free HBM holds, agreed
+    over the ranks by `gather` (xdist.gather_seconds: one value per rank) --
+    and rank r takes the contiguous range xdist.stripe_range(total, r, world).
+    At 8 ranks and 8,192 requested: 65,536 stripes, 8,192 per GPU."""
+    mine = float(min(requested, fits))
+    per_rank = int(min(gather(mine) if gather else [mine]))
+    total = per_rank * world
+    first, n = xdist.stripe_range(total, rank, world) if per_rank > 0 else (0, 0)
+    return {"per_rank": per_rank, "total": total, "first": first, "n": n}
+
+
 def config5(R: Rank, args):
     """BASELINE config 5: Encode and ReconstOne of 1 MiB stripes, a fixed
     number per rank (8,192 = 128 GiB per GPU; 65,536 stripes = 1 TiB over 8),
@@ -521,11 +534,11 @@ def config5(R: Rank, args):
     # emptiest GPU's free HBM holds (minus 4 GiB), agreed over the ranks.
     free, _ = torch.cuda.mem_get_info()
     fits = max(0, (free - (4 << 30)) // stripe)
-    per_rank = int(min(xdist.gather_seconds(float(min(args.config5_stripes, fits)), R.tdev)))
-    if per_rank < 1:
+    plan = config5_plan(args.config5_stripes, fits, w.rank, w.world,
+                        lambda v: xdist.gather_seconds(v, R.tdev))
+    if plan["per_rank"] < 1:
         return {"skipped": f"no room for one 16 MiB stripe ({free / GIB:.1f} GiB free)"}
-    total = per_rank * w.world
-    first, n = xdist.stripe_range(total, w.rank, w.world)
+    total, first, n = plan["total"], plan["first"], plan["n"]
     t0 = time.perf_counter()
     buf = R.random_bytes(n * stripe, 0xC05 + first)
     base = buf.data_ptr()
@@ -634,9 +647,33 @@ def config4(R: Rank, args):
 
 def host_e2e(R: Rank, args):
     """Shards start and end in host memory: pinned, device-mapped batches
-    (xrs_host_alloc) run in place over PCIe by xrs_encode_host /
-    xrs_reconst_one_host, every rank at once over its own link.  Reference
-    call sites: xrs.go:103-128 (Encode), :175-221 (ReconstOne)."""
+    (xrs_host_alloc) run by xrs_encode_host / xrs_reconst_one_host, every rank
+    at once over its own link, two ways:
+      * top-level keys: in place over PCIe (the kernels read and write the
+        pinned batch through its device address; the default);
+      * "dma": the north star's "pinned hipMemcpyAsync in and out" -- the same
+        batches with XRS_HOST_ZC=0, i.e. 64 MiB chunks through three device
+        slots and streams, H2D / kernel / D2H overlapped (codec.cpp
+        run_pipeline); ReconstOne moves only its need set.
+    Reference call sites: xrs.go:103-128 (Encode), :175-221 (ReconstOne)."""
+    out = _host_e2e_pass(R, args)
+    out["path"] = "pinned host memory, kernels in place over PCIe (xrs_*_host zero-copy)"
+    prev = os.environ.get("XRS_HOST_ZC")
+    os.environ["XRS_HOST_ZC"] = "0"  # read per call (codec.cpp host_zero_copy)
+    try:
+        dma = _host_e2e_pass(R, args)
+    finally:
+        if prev is None:
+            del os.environ["XRS_HOST_ZC"]
+        else:
+            os.environ["XRS_HOST_ZC"] = prev
+    dma["path"] = ("pinned host memory, hipMemcpy2DAsync H2D -> kernel -> D2H over three "
+                   "streams in 64 MiB chunks (XRS_HOST_ZC=0)")
+    out["dma"] = dma
+    return out
+
+
+def _host_e2e_pass(R: Rank, args):
     import ctypes
 
     import numpy as np
@@ -667,7 +704,38 @@ def host_e2e(R: Rank, args):
                         "gibps": round(algo * 3 * R.w.world / max(secs) / GIB, 2)}
         finally:
             L.xrs_host_free(ptr)
-    out["path"] = "pinned host memory, kernels in place over PCIe (xrs_*_host zero-copy)"
+    return out
+
+
+XGMI_PLACEMENTS = {"half": lambda dev, ndev, i: dev if i % 2 == 0 else (dev + 1) % ndev,
+                   "spread": lambda dev, ndev, i: (dev + i) % ndev}
+
+
+def xgmi_need_plan(dev: int, ndev: int, k: int, size: int, n: int, a_need, b_need) -> dict:
+    """Which need-set bytes of ReconstOne(k) (GetNeedVects, xrs.go:146-171;
+    read set xrs.go:175-221) each placement puts on a peer GPU (no GPU call):
+    the b-halves of the d - 1 surviving data vects, of parity d and of parity
+    bi, and the a-halves of aNeed.  Per layout: the shards read, how many
+    live on a peer, and the bytes the kernel on `dev` reads over xGMI per
+    call (n stripes)."""
+    half = size // 2
+    halves = {}  # shard -> halves read per stripe
+    for m in range(D):
+        if m != k:
+            halves[m] = halves.get(m, 0) + 1
+    for b in b_need:
+        halves[b] = halves.get(b, 0) + 1
+    for a in a_need:
+        halves[a] = halves.get(a, 0) + 1
+    out = {}
+    for name, place in XGMI_PLACEMENTS.items():
+        remote = {i: c for i, c in halves.items() if place(dev, ndev, i) != dev}
+        out[name] = {
+            "need_set_shards": len(halves), "need_set_shards_remote": len(remote),
+            "need_set_bytes": n * half * sum(halves.values()),
+            "need_set_bytes_remote": n * half * sum(remote.values()),
+            "gpus_read": sorted({place(dev, ndev, i) for i in halves}),
+        }
     return out
 
 
@@ -697,7 +765,7 @@ def xgmi_repair(R: Rank, args):
     R.sync()
     expect = local[k * col:(k + 1) * col].clone()
     a_need, b_need = x.get_need_vects(k)
-    need = sorted(set([m for m in range(D) if m != k] + b_need + a_need))
+    plan = xgmi_need_plan(dev, ndev, k, size, n, a_need, b_need)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def rate(table):
@@ -711,8 +779,7 @@ def xgmi_repair(R: Rank, args):
         R.sync()
         return round(n * 9 * size / (e0.elapsed_time(e1) / reps / 1e3) / 1e9, 1)
 
-    placements = {"half": lambda i: dev if i % 2 == 0 else (dev + 1) % ndev,
-                  "spread": lambda i: (dev + i) % ndev}
+    placements = {name: (lambda i, f=f: f(dev, ndev, i)) for name, f in XGMI_PLACEMENTS.items()}
     out = {"device": dev, "gpus_visible": ndev, "stripes": n, "vect_bytes": size, "k": k,
            "bytes_per_call": n * 9 * size, "layouts": {}}
     exact_all = True
@@ -730,15 +797,12 @@ def xgmi_repair(R: Rank, args):
         gbs = rate(table)
         exact = exact and bool(torch.equal(local[k * col:(k + 1) * col], expect))
         exact_all = exact_all and exact
-        out["layouts"][name] = {
-            "need_set_shards_remote": sum(1 for i in need if place(i) != dev),
-            "need_set_shards": len(need),
-            "gpus_read": sorted({place(i) for i in need}), "gbs_algorithmic": gbs,
-            "bitexact": exact}
+        out["layouts"][name] = dict(plan[name], gbs_algorithmic=gbs, bitexact=exact)
         del copies, table
         torch.cuda.empty_cache()
     out["gbs_all_local"] = rate([local.data_ptr() + i * col for i in range(D + P)])
     out["gbs_algorithmic"] = out["layouts"]["half"]["gbs_algorithmic"]
+    out["need_set_bytes_remote"] = out["layouts"]["half"]["need_set_bytes_remote"]
     out["xgmi_bitexact"] = exact_all
     del local, expect
     torch.cuda.empty_cache()

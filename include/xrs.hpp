@@ -247,6 +247,46 @@ class Queue {
                                        static_cast<int>(p.size())),
                       row);
   }
+  // Asynchronous Encode / ReconstOne (xrs_queue_submit_*): the stripe is
+  // staged now and *t set; t->Wait() blocks until it is done and returns the
+  // call's error.  The vects must not be touched until then.  A submit that
+  // finds every staging batch held by unwaited tickets returns the "queue
+  // busy" error with nothing staged: Wait on an earlier ticket and resubmit.
+  class Ticket {
+   public:
+    Ticket() = default;
+    Ticket(const Ticket&) = delete;
+    Ticket& operator=(const Ticket&) = delete;
+    ~Ticket() { (void)Wait(); }
+    bool Done() const { return !t_ || xrs_queue_poll(t_) == 1; }
+    Error Wait() {
+      if (!t_) return {};
+      const int rc = xrs_queue_wait(t_);
+      t_ = nullptr;
+      return make_error(rc, arg_);
+    }
+
+   private:
+    friend class Queue;
+    xrs_queue_ticket* t_ = nullptr;
+    long long arg_ = 0;
+  };
+  Error SubmitEncode(std::vector<Slice> vects, Ticket* t) {
+    (void)t->Wait();
+    auto p = ptrs(vects);
+    if (!same_len(vects, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
+    t->arg_ = static_cast<long long>(size_);
+    return make_error(xrs_queue_submit_encode(q_, p.data(), static_cast<int>(p.size()), &t->t_),
+                      t->arg_);
+  }
+  Error SubmitReconstOne(std::vector<Slice> vects, int k, Ticket* t) {
+    (void)t->Wait();
+    auto p = ptrs(vects);
+    if (!same_len(vects, size_)) return make_error(XRS_ERR_ILLEGAL_VECTS);
+    t->arg_ = k;
+    return make_error(xrs_queue_submit_reconst_one(q_, p.data(), static_cast<int>(p.size()), k, &t->t_),
+                      k);
+  }
   // Batches run so far by stripe count (xrs_queue_batch_sizes): element n =
   // batches of n stripes, the last element = batches of 64 or more.
   std::vector<uint64_t> BatchSizes() const {

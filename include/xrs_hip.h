@@ -43,6 +43,7 @@ extern "C" {
 #define XRS_ERR_HIP (-8)                /* HIP runtime failure                    */
 #define XRS_ERR_INVALID_ARG (-9)        /* NULL pointer / bad layout argument     */
 #define XRS_ERR_NO_DEVICE (-10)         /* no GPU visible                         */
+#define XRS_ERR_BUSY (-11)              /* xrs_queue_submit_*: no staging batch free */
 
 typedef struct xrs_codec xrs_codec;
 
@@ -211,10 +212,23 @@ int xrs_replace_host(const xrs_codec *codec, const uint8_t *data_base, size_t da
                      size_t data_stripe_stride, const int *rows, int n, size_t size,
                      uint8_t *parity_base, size_t parity_shard_stride,
                      size_t parity_stripe_stride, size_t n_stripes);
+/* Pinned, device-mapped host memory.  Per-stripe calls (xrs_encode ...,
+ * xrs_queue_* and xrs_queue_submit_*) whose every vect lies in such memory
+ * do not copy: the kernels read and write the caller's buffers IN PLACE over
+ * PCIe (codec.cpp reg_vects, queue.cpp table mode), host-resident batches
+ * (*_host) likewise.  Lifetime contract: xrs_host_free / xrs_host_unregister
+ * only when no call on vects inside the range is in flight (a synchronous
+ * call has returned; every ticket of an asynchronous one has been waited
+ * on).  After unregister the pages are ordinary pageable memory again: they
+ * may be freed and reused, and later pageable copies from them are exact
+ * (tests/cpp/xrs_test.cpp TestRegistered_UnregisterFreeReuse,
+ * tests/test_gpu_registered.py::test_unregister_free_reuse_then_pageable_copy).
+ * Registering is a pin and a map (tens of us per MiB), so a buffer pool that
+ * registers once and lives long is the intended use. */
 void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */
 void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */
-int xrs_host_unregister(void *p);
+int xrs_host_unregister(void *p);             /* p: the pointer given to xrs_host_register */
 /* Device address of pinned, mapped host memory (from xrs_host_alloc or
  * xrs_host_register), or NULL.  It may be passed as the base of the
  * *_batched calls: the kernels then read and write host memory over PCIe
@@ -287,6 +301,32 @@ int xrs_queue_replace(xrs_queue *q, uint8_t *const *data, const int *rows, int n
 /* xrs.go:324 Update(oldData, newData, row, parity), coalesced. */
 int xrs_queue_update(xrs_queue *q, const uint8_t *old_data, const uint8_t *new_data, int row,
                      uint8_t *const *parity, int n_parity);
+/* Asynchronous forms (one caller thread -- one cgo call site -- keeps several
+ * stripes in flight; reference call pattern xrs_test.go:498-521, one
+ * x.Encode per stripe).  A submit validates like the synchronous call, stages
+ * the stripe into the open batch and returns at once with *ticket set;
+ * xrs_queue_wait(ticket) blocks until that stripe is done, copies its outputs
+ * back (vects outside registered memory), frees the ticket and returns the
+ * call's status.  The vects must stay valid and must not be touched until the
+ * wait returns.  Every ticket is waited on exactly once, before
+ * xrs_queue_free.  A submit never blocks: with no staging batch free it
+ * returns XRS_ERR_BUSY and stages nothing -- wait on one of your tickets
+ * (e.g. the oldest) and submit again.  A Reconst the queue cannot batch
+ * (see xrs_queue_reconst) runs at once and returns a finished ticket. */
+typedef struct xrs_queue_ticket xrs_queue_ticket;
+int xrs_queue_submit_encode(xrs_queue *q, uint8_t *const *vects, int n, xrs_queue_ticket **ticket);
+int xrs_queue_submit_reconst_one(xrs_queue *q, uint8_t *const *vects, int n, int k,
+                                 xrs_queue_ticket **ticket);
+int xrs_queue_submit_reconst(xrs_queue *q, uint8_t *const *vects, int n, const int *dp_has,
+                             int n_has, const int *need, int n_need, xrs_queue_ticket **ticket);
+int xrs_queue_submit_replace(xrs_queue *q, uint8_t *const *data, const int *rows, int n,
+                             uint8_t *const *parity, int n_parity, xrs_queue_ticket **ticket);
+int xrs_queue_submit_update(xrs_queue *q, const uint8_t *old_data, const uint8_t *new_data,
+                            int row, uint8_t *const *parity, int n_parity,
+                            xrs_queue_ticket **ticket);
+/* 1 when the ticket's stripe is done (xrs_queue_wait will not block), else 0. */
+int xrs_queue_poll(const xrs_queue_ticket *ticket);
+int xrs_queue_wait(xrs_queue_ticket *ticket);
 size_t xrs_queue_batch_stripes(const xrs_queue *q);
 /* Counters since xrs_queue_new: out[0] batches run, out[1] stripes run,
  * out[2] ns from each batch's launch to its completion, out[3] ns each batch

@@ -4,6 +4,7 @@
 //
 //   xrs_test --cpu   host-logic tests only (no GPU needed)
 //   xrs_test         all tests (needs the MI355X)
+//   xrs_test NAME..  only the named tests
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -14,6 +15,8 @@
 #include <string>
 #include <thread>
 
+#include <hip/hip_runtime_api.h>
+
 #include "xrs.hpp"
 
 using xrs::Error;
@@ -22,6 +25,16 @@ using xrs::Vects;
 using xrs::XRS;
 
 static int g_fail = 0;
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define XRS_TEST_ASAN 1
+#endif
+#endif
+#if defined(__SANITIZE_ADDRESS__) || defined(XRS_TEST_ASAN)
+static constexpr bool kAsanBuild = true;
+#else
+static constexpr bool kAsanBuild = false;
+#endif
 #define FATAL(...)                          \
   do {                                      \
     std::printf("FAIL %s: ", __func__);     \
@@ -299,6 +312,65 @@ static void TestQueue_Concurrent() {
   if (Error e = q->Update(Vect(kShard), Vect(kShard), kData, xrs::slices(par));
       !e || e.msg != "illegal data index: 12")
     FATAL("Update(row=d): got \"%s\"", e.msg.c_str());
+}
+
+// Not in the reference: the asynchronous queue calls.  8 threads, each keeping
+// a window of 6 stripes in flight (xrs::Queue::SubmitEncode /
+// SubmitReconstOne, then Ticket::Wait oldest first; a "queue busy" submit
+// waits on the oldest ticket and retries), every stripe equal to a second
+// codec's synchronous call.  One cgo call site with k stripes outstanding
+// (the reference's call, xrs_test.go:498-521, is one x.Encode per stripe).
+static void TestQueue_Async() {
+  constexpr int kThreads = 8, kWin = 6, kStripes = 48, kSize = 4096;
+  auto x = must_new(kData, kParity), y = must_new(kData, kParity);
+  std::unique_ptr<xrs::Queue> q;
+  if (Error e = xrs::Queue::New(*x, kSize, &q, 8, 50)) FATAL("Queue::New: %s", e.msg.c_str());
+  std::atomic<int> bad{0}, busy{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < kThreads; ++t)
+    th.emplace_back([&, t] {
+      std::mt19937_64 r(900 + t);
+      std::vector<Vects> v(kStripes, new_shard_matrix(kData + kParity, kSize));
+      std::vector<Vects> ref(kStripes);
+      for (int s = 0; s < kStripes; ++s) {
+        for (int j = 0; j < kData; ++j) fill_random(r, v[s][j]);
+        ref[s] = v[s];
+        if (y->Encode(ref[s])) ++bad;
+      }
+      std::vector<int> ks(kStripes);
+      for (int& k : ks) k = static_cast<int>(r() % kData);
+      for (int pass = 0; pass < 2; ++pass) {
+        std::vector<xrs::Queue::Ticket> tk(kStripes);
+        int oldest = 0;
+        for (int s = 0; s < kStripes; ++s) {
+          if (s - oldest >= kWin && tk[oldest++].Wait()) ++bad;
+          for (;;) {
+            Error e = pass == 0 ? q->SubmitEncode(xrs::slices(v[s]), &tk[s])
+                                : q->SubmitReconstOne(xrs::slices(v[s]), ks[s], &tk[s]);
+            if (!e) break;
+            if (e.msg != "queue busy") {
+              ++bad;
+              break;
+            }
+            ++busy;
+            if (oldest < s) {
+              if (tk[oldest++].Wait()) ++bad;
+            } else {
+              std::this_thread::yield();
+            }
+          }
+        }
+        for (; oldest < kStripes; ++oldest)
+          if (tk[oldest].Wait()) ++bad;
+        for (int s = 0; s < kStripes; ++s)
+          if (v[s] != ref[s]) ++bad;
+        if (pass == 0)
+          for (int s = 0; s < kStripes; ++s) std::fill(v[s][ks[s]].begin(), v[s][ks[s]].end(), 0);
+      }
+    });
+  for (auto& t : th) t.join();
+  std::printf("  async: %d busy returns\n", busy.load());
+  if (bad) FATAL("%d mismatches or errors", bad.load());
 }
 
 // Not in the reference: 32 threads released together (a spin barrier) make
@@ -617,6 +689,97 @@ static void TestRegistered_SyncAndQueue() {
   if (bad) FATAL("%d mismatches or errors", bad.load());
 }
 
+// Registered pages handed back and reused.  A buffer is
+// pinned with xrs_host_register, an in-place Encode runs on it (xrs.go:103-128,
+// the call whose buffers a cgo BufPool pools), then it is unregistered and
+// freed, and the allocator hands the same pages out again -- what a Go
+// BufPool.Close() followed by GC and new allocations does.
+// On the reused pages: the runtime's pageable copies (hipMemcpy H2D from
+// them and D2H into them) and a pageable host-resident Encode
+// (xrs_encode_host, hipMemcpy2DAsync chunks) must be exact and leave no
+// error.  64 KiB buffers come from the heap, 2 MiB ones first from mmap.
+static void TestRegistered_UnregisterFreeReuse() {
+  constexpr size_t S = 4096, kStripe = (kData + kParity) * S;  // 64 KiB
+  auto x = must_new(kData, kParity);
+  std::mt19937_64 r(4242);
+  int reused = 0, rounds = 0;
+  uint8_t* dev = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&dev), size_t(2) << 20) != hipSuccess) FATAL("hipMalloc");
+  auto overlaps = [](const uint8_t* a, const uint8_t* b, size_t n) { return b < a + n && a < b + n; };
+  auto encoded_copy = [&](const uint8_t* base, size_t n_stripes) {
+    Vects all;
+    for (size_t s = 0; s < n_stripes; ++s) {
+      Vects v = new_shard_matrix(kData + kParity, S);
+      for (int j = 0; j < kData + kParity; ++j) std::memcpy(v[j].data(), base + s * kStripe + j * S, S);
+      if (x->Encode(v)) return Vects();
+      for (auto& e : v) all.push_back(std::move(e));
+    }
+    return all;
+  };
+  auto same = [&](const Vects& want, const uint8_t* base) {
+    if (want.empty()) return false;
+    for (size_t i = 0; i < want.size(); ++i)
+      if (std::memcmp(want[i].data(), base + i * S, S)) return false;
+    return true;
+  };
+  for (size_t bytes : {kStripe, size_t(2) << 20}) {
+    const size_t n_stripes = bytes / kStripe;
+    for (int round = 0; round < 8; ++round, ++rounds) {
+      // 1. register a page-aligned malloc buffer; Encode in place on it
+      uint8_t* a = static_cast<uint8_t*>(std::aligned_alloc(4096, bytes));
+      for (size_t i = 0; i < bytes; ++i) a[i] = static_cast<uint8_t>(r());
+      const Vects want_a = encoded_copy(a, 1);
+      if (xrs_host_register(a, bytes)) FATAL("xrs_host_register");
+      std::vector<uint8_t*> v(kData + kParity);
+      for (int j = 0; j < kData + kParity; ++j) v[j] = a + j * S;
+      if (xrs_encode(x->codec(), v.data(), kData + kParity, S) || !same(want_a, a))
+        FATAL("in-place Encode on registered memory, round %d", round);
+      // 2. unregister, free
+      if (xrs_host_unregister(a)) FATAL("xrs_host_unregister");
+      std::free(a);
+      // 3. allocate until the allocator hands back a page of the old buffer
+      uint8_t* b = nullptr;
+      std::vector<uint8_t*> held;
+      for (int t = 0; t < 32 && !b; ++t) {
+        uint8_t* c = static_cast<uint8_t*>(std::aligned_alloc(4096, bytes));
+        if (overlaps(a, c, bytes)) b = c;
+        else held.push_back(c);
+      }
+      if (b) ++reused;
+      else {
+        b = held.back();
+        held.pop_back();
+      }
+      for (uint8_t* h : held) std::free(h);
+      // 4. the runtime's pageable copies to and from the reused pages
+      for (size_t i = 0; i < bytes; ++i) b[i] = static_cast<uint8_t>(r());
+      std::vector<uint8_t> back(bytes), keep(b, b + bytes);
+      if (hipMemcpy(dev, b, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(back.data(), dev, bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+          std::memcmp(back.data(), b, bytes))
+        FATAL("pageable H2D from reused pages, %zu B, round %d", bytes, round);
+      std::memset(b, 0, bytes);
+      if (hipMemcpy(b, dev, bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+          std::memcmp(keep.data(), b, bytes))
+        FATAL("pageable D2H into reused pages, %zu B, round %d", bytes, round);
+      // 5. a pageable host-resident Encode over them
+      const Vects want_b = encoded_copy(b, n_stripes);
+      if (xrs_encode_host(x->codec(), b, S, S, kStripe, n_stripes) || !same(want_b, b))
+        FATAL("xrs_encode_host on reused pages, %zu B, round %d", bytes, round);
+      if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess)
+        FATAL("HIP error after round %d", round);
+      std::free(b);
+    }
+  }
+  (void)hipFree(dev);
+  std::printf("  unregister -> free -> reuse: a freed page came back in %d of %d rounds\n", reused,
+              rounds);
+  // (ASan's allocator quarantines freed memory, so its build never sees reuse:
+  // there the test checks only the copies and the Encodes)
+  if (reused == 0 && !kAsanBuild)
+    FATAL("the allocator never reused a freed registered page: the test tested nothing");
+}
+
 static void TestMismatchedVects() {
   std::unique_ptr<XRS> x;
   if (Error e = XRS::New(kData, kParity, &x)) FATAL("New: %s", e.msg.c_str());
@@ -642,7 +805,13 @@ static void TestMismatchedVects() {
 }
 
 int main(int argc, char** argv) {
-  const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
+  // xrs_test [--cpu] [name ...]: host-logic tests only, and/or only the named tests
+  bool cpu_only = false;
+  std::vector<std::string> only;
+  for (int i = 1; i < argc; ++i) {
+    if (std::strcmp(argv[i], "--cpu") == 0) cpu_only = true;
+    else only.push_back(argv[i]);
+  }
   struct T {
     const char* name;
     void (*fn)();
@@ -660,12 +829,15 @@ int main(int argc, char** argv) {
       {"TestQueue_Concurrent", TestQueue_Concurrent, true},
       {"TestQueue_Oversubscribed", TestQueue_Oversubscribed, true},
       {"TestQueue_Coalesces", TestQueue_Coalesces, true},
+      {"TestQueue_Async", TestQueue_Async, true},
       {"TestXRS_SharedCodecConcurrent", TestXRS_SharedCodecConcurrent, true},
       {"TestXRS_ReconstPersistent", TestXRS_ReconstPersistent, true},
       {"TestRegistered_SyncAndQueue", TestRegistered_SyncAndQueue, true},
+      {"TestRegistered_UnregisterFreeReuse", TestRegistered_UnregisterFreeReuse, true},
   };
   for (const T& t : tests) {
     if (cpu_only && t.gpu) continue;
+    if (!only.empty() && std::find(only.begin(), only.end(), t.name) == only.end()) continue;
     const int before = g_fail;
     t.fn();
     std::printf("%s %s\n", g_fail == before ? "ok  " : "FAIL", t.name);

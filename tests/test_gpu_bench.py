@@ -64,7 +64,9 @@ def test_bench_one_gpu_contract():
     c5 = j["config5"]
     assert c5["stripes_total"] == 64 and c5["stripes_per_rank"] == 64 and c5["roundtrip_ok"]
     assert len(c5["encode"]["rank_seconds"]) == 1 and c5["gibps"] > 0
-    assert set(j["host_e2e"]) >= {"encode_4k", "reconst_one_1m"}
+    assert set(j["host_e2e"]) >= {"encode_4k", "reconst_one_1m", "dma"}
+    assert set(j["host_e2e"]["dma"]) >= {"encode_4k", "reconst_one_1m", "path"}
+    assert j["host_e2e"]["dma"]["encode_4k"]["gibps"] > 0
     xg = j["xgmi_repair"]
     assert ("skipped" in xg) or xg["xgmi_bitexact"], xg
 

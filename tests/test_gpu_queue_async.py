@@ -1,0 +1,225 @@
+"""GPU tests of the batching queue's asynchronous forms (xrs_queue_submit_* /
+xrs_queue_wait / xrs_queue_poll): one caller thread keeps many stripes in
+flight (the cgo call site that submits k stripes, then waits), every kind of
+call bit-exact to the oracle (oracle/xrs_oracle.c, following xrs.go:103-387),
+on plain and on registered vects, and XRS_ERR_BUSY when every staging batch
+holds unwaited tickets.  Reference call pattern: xrs_test.go:498-521."""
+import ctypes
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import xrs_amd
+from oracle.oracle_c import OracleXRS
+
+pytestmark = pytest.mark.gpu
+D, P = 12, 4
+
+
+def _same(a, b):
+    return all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("size", [4096, 1030, 1 << 20])
+def test_async_one_thread_every_op(size):
+    """One thread submits a window of stripes of one kind, then waits on
+    them oldest first; Encode, ReconstOne (garbage outside the need set),
+    Update, Replace(2) and a clean Reconst (2 lost, with the retrieveRS side
+    effect), each vs the oracle."""
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=16)
+    rng = np.random.Generator(np.random.PCG64(size))
+    n = 24 if size < (1 << 20) else 6
+
+    def run(tickets):
+        for t in tickets:
+            assert t is not None
+            t.wait()
+
+    stripes = [[rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+               for _ in range(n)]
+    refs = [[a.copy() for a in v] for v in stripes]
+    for r in refs:
+        o.encode(r)
+    run([q.submit_encode(v) for v in stripes])
+    assert all(_same(v, r) for v, r in zip(stripes, refs)), "encode"
+    # ReconstOne(k), k per stripe
+    ks = [int(rng.integers(0, D)) for _ in range(n)]
+    for v, k in zip(stripes, ks):
+        a_need, _ = x.get_need_vects(k)
+        v[k][:] = 0
+        for j in range(D + P):
+            if j not in a_need and j != k:
+                v[j][: size // 2] = 0xC3
+    run([q.submit_reconst_one(v, k) for v, k in zip(stripes, ks)])
+    assert all(np.array_equal(v[k], r[k]) for v, r, k in zip(stripes, refs, ks)), "reconst_one"
+    for v, r in zip(stripes, refs):
+        for j in range(D + P):
+            v[j][:] = r[j]
+    # Update(row) with fresh data
+    news = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(n)]
+    rows = [int(rng.integers(0, D)) for _ in range(n)]
+    run([q.submit_update(v[row], new, row, v[D:]) for v, new, row in zip(stripes, news, rows)])
+    for r, new, row in zip(refs, news, rows):
+        o.update(r[row], new, row, r[D:])
+        r[row][:] = new
+    for v, new, row in zip(stripes, news, rows):
+        v[row][:] = new
+    assert all(_same(v, r) for v, r in zip(stripes, refs)), "update"
+    # Replace(rows 1, 7)
+    datas = [[rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(2)] for _ in range(n)]
+    run([q.submit_replace(dd, [1, 7], v[D:]) for v, dd in zip(stripes, datas)])
+    for r, dd in zip(refs, datas):
+        o.replace(dd, [1, 7], r[D:])
+    assert all(_same(v[D:], r[D:]) for v, r in zip(stripes, refs)), "replace"
+    # Reconst of two lost data vects (clean: batched)
+    lost = [3, 9]
+    has = [i for i in range(D + P) if i not in lost]
+    for v, r in zip(stripes, refs):
+        for j in lost:
+            v[j][:] = 0x5A
+            r[j][:] = 0x5A
+        o.reconst(r, has, lost)
+    run([q.submit_reconst(v, has, lost) for v in stripes])
+    assert all(_same(v, r) for v, r in zip(stripes, refs)), "reconst"
+    # an unclean Reconst (repeated index) runs at once: a finished ticket
+    v, r = stripes[0], [a.copy() for a in stripes[0]]
+    t = q.submit_reconst(v, has + [has[0]], lost)
+    assert t.done()
+    t.wait()
+    x.reconst(r, has + [has[0]], lost)
+    assert _same(v, r)
+    st = q.stats()
+    assert st["batches"] < st["stripes"]  # a window of submits shares batches
+    q.close()
+
+
+def test_async_busy_then_wait_and_resubmit():
+    """With every staging batch holding unwaited tickets a submit returns
+    XRS_ERR_BUSY (None here) at once, staging nothing; after waiting on the
+    oldest ticket the same submit goes through.  Every stripe vs the oracle."""
+    size = 4096
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=2)
+    rng = np.random.Generator(np.random.PCG64(5))
+    n = 64
+    stripes = [[rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
+               for _ in range(n)]
+    refs = [[a.copy() for a in v] for v in stripes]
+    for r in refs:
+        o.encode(r)
+    pending, busy = [], 0
+    for v in stripes:
+        while True:
+            t = q.submit_encode(v)
+            if t is not None:
+                pending.append(t)
+                break
+            busy += 1
+            pending.pop(0).wait()
+    for t in pending:
+        t.wait()
+    assert busy > 0  # 6 staging batches of 2 stripes cannot hold 64 tickets
+    assert all(_same(v, r) for v, r in zip(stripes, refs))
+    assert q.stats()["stripes"] == n
+    q.close()
+
+
+def test_async_c_abi_threads_registered_and_plain():
+    """8 threads, each keeping a window of 8 Encode stripes in flight through
+    the C ABI (pointer arrays made beforehand), half of them on registered
+    vects (xrs_host_alloc: table mode, in place); then ReconstOne the same
+    way.  Every stripe vs the oracle; xrs_queue_poll agrees with the wait."""
+    size, win, per = 4096, 8, 32
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    q = xrs_amd.XRSQueue(x, size, max_batch_stripes=32)
+    L, qh = xrs_amd.lib(), q.handle
+    errors = []
+    pinned = []
+
+    def worker(t):
+        rng = np.random.Generator(np.random.PCG64(300 + t))
+        try:
+            if t % 2:  # registered: one xrs_host_alloc arena per thread
+                nbytes = per * (D + P) * size
+                ptr = L.xrs_host_alloc(nbytes)
+                assert ptr
+                pinned.append(ptr)
+                arena = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
+                vs = [[arena[(s * (D + P) + j) * size:(s * (D + P) + j + 1) * size]
+                       for j in range(D + P)] for s in range(per)]
+            else:
+                vs = [[np.empty(size, np.uint8) for _ in range(D + P)] for _ in range(per)]
+            for v in vs:
+                for a in v:
+                    a[:] = rng.integers(0, 256, size=size, dtype=np.uint8)
+            refs = [[a.copy() for a in v] for v in vs]
+            for r in refs:
+                o.encode(r)
+            arrs = [(ctypes.c_void_p * (D + P))(*[a.ctypes.data for a in v]) for v in vs]
+
+            def window(submit):
+                live = []
+                for s in range(per):
+                    while True:
+                        tk = ctypes.c_void_p()
+                        rc = submit(s, ctypes.byref(tk))
+                        if rc == 0:
+                            live.append(tk)
+                            break
+                        assert rc == xrs_amd.XRS_ERR_BUSY, rc
+                        if live:  # wait on our oldest, else on the other callers
+                            assert L.xrs_queue_wait(live.pop(0)) == 0
+                        else:
+                            time.sleep(1e-4)
+                    if len(live) >= win:
+                        assert L.xrs_queue_wait(live.pop(0)) == 0
+                for tk in live:
+                    L.xrs_queue_wait(tk) == 0 or errors.append("wait")
+
+            window(lambda s, tp: L.xrs_queue_submit_encode(qh, arrs[s], D + P, tp))
+            if not all(_same(v, r) for v, r in zip(vs, refs)):
+                errors.append(("encode", t))
+            ks = [int(rng.integers(0, D)) for _ in range(per)]
+            for v, k in zip(vs, ks):
+                v[k][:] = 0
+            window(lambda s, tp: L.xrs_queue_submit_reconst_one(qh, arrs[s], D + P, ks[s], tp))
+            if not all(np.array_equal(v[k], r[k]) for v, r, k in zip(vs, refs, ks)):
+                errors.append(("reconst_one", t))
+            # poll: a finished ticket reads 1 before its wait
+            tk = ctypes.c_void_p()
+            assert L.xrs_queue_submit_encode(qh, arrs[0], D + P, ctypes.byref(tk)) in (0, -11)
+            if tk.value:
+                while L.xrs_queue_poll(tk) != 1:
+                    pass
+                assert L.xrs_queue_wait(tk) == 0
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    alive = any(t.is_alive() for t in th)
+    dump = q.dump() if alive else ""
+    q.close()
+    for ptr in pinned:
+        L.xrs_host_free(ptr)
+    assert not alive, "a caller hung:\n" + dump
+    assert not errors, errors[:3]
+
+
+def test_async_errors():
+    x = xrs_amd.XRS(D, P)
+    q = xrs_amd.XRSQueue(x, 64)
+    with pytest.raises(xrs_amd.XRSError, match="illegal data index: 12"):
+        q.submit_reconst_one([np.zeros(64, np.uint8) for _ in range(16)], 12)
+    L = xrs_amd.lib()
+    assert L.xrs_queue_wait(None) == xrs_amd.XRS_ERR_INVALID_ARG
+    assert L.xrs_queue_poll(None) == xrs_amd.XRS_ERR_INVALID_ARG
+    arr = (ctypes.c_void_p * 16)()
+    assert L.xrs_queue_submit_encode(q.handle, arr, 16, None) == xrs_amd.XRS_ERR_INVALID_ARG
+    q.close()

@@ -22,7 +22,6 @@ pytestmark = pytest.mark.gpu
 
 D, P = 12, 4
 PAGE = 4096
-_RETIRED = []  # unregistered arenas, kept alive (Arena.close)
 
 
 class Arena:
@@ -76,9 +75,10 @@ class Arena:
             L.xrs_host_free(self.ptr)
         else:
             assert L.xrs_host_unregister(self.ptr) == 0
-            # keep the pages for the session: later buffers (and the runtime's
-            # pageable copies from them) do not land on just-unpinned pages
-            _RETIRED.append(self.raw)
+            # the pages go back to numpy's allocator, so later buffers (and the
+            # runtime's pageable copies from them) may land on them: what a Go
+            # BufPool.Close() followed by GC does
+        self.raw = self.buf = None
 
 
 def _ind_launches(tr):
@@ -420,3 +420,56 @@ def test_registered_fuzz_vs_oracle(seed, via):
         assert _ind_launches(tr) > 0, tr
     else:
         assert tr.get("host:sync_in_place", 0) > 0, tr
+
+
+@pytest.mark.parametrize("nbytes", [64 << 10, 2 << 20])
+def test_unregister_free_reuse_then_pageable_copy(nbytes):
+    """register -> in-place Encode -> unregister -> free -> the allocator hands
+    the pages out again -> PyTorch's pageable copies from and into them (the
+    copy at which the reverted groups-of-12 build's illegal-address error
+    surfaced, profiles/r05_g12_diag.log).  Bytes exact, no HIP error; the
+    C++ twin is tests/cpp/xrs_test.cpp TestRegistered_UnregisterFreeReuse.
+    Reference call on the pooled buffers: xrs.go:103-128."""
+    import gc
+
+    import torch
+
+    L = xrs_amd.lib()
+    x, o = xrs_amd.XRS(D, P), OracleXRS(D, P)
+    rng = np.random.Generator(np.random.PCG64(nbytes))
+    size = 4096
+    reused = 0
+    for _ in range(4):
+        ar = Arena(nbytes, "register")
+        lo, hi = ar.ptr, ar.ptr + nbytes
+        v = [ar.take(size) for _ in range(D + P)]
+        _fill(rng, v[:D])
+        want = [a.copy() for a in v]
+        o.encode(want)
+        x.encode(v)
+        assert _same(v, want)
+        del v
+        ar.close()
+        del ar
+        gc.collect()
+        # fresh buffers of the same size until one overlaps the freed pages
+        held, hit = [], None
+        for _ in range(16):
+            b = np.empty(nbytes + PAGE, np.uint8)
+            if b.ctypes.data < hi and lo < b.ctypes.data + b.nbytes:
+                hit = b
+                break
+            held.append(b)
+        reused += hit is not None
+        b = hit if hit is not None else np.empty(nbytes + PAGE, np.uint8)
+        del held
+        b[:] = rng.integers(0, 256, size=b.nbytes, dtype=np.uint8)
+        t = torch.from_numpy(b).to("cuda:0")  # pageable H2D
+        back = t.cpu()                         # pageable D2H
+        torch.cuda.synchronize()
+        assert np.array_equal(back.numpy(), b)
+        keep = b.copy()
+        b[:] = 0
+        b[:] = t.cpu().numpy()
+        assert np.array_equal(b, keep)
+    assert reused, "numpy never handed a freed registered page out again"

@@ -36,7 +36,7 @@ BUDGETS = [
 ]
 
 
-def _notes(tmp_path):
+def _code_objects(tmp_path):
     for tool in ("objcopy",):
         if not shutil.which(tool):
             pytest.skip(f"{tool} not available")
@@ -57,7 +57,7 @@ def _notes(tmp_path):
         starts.append(i)
         i = data.find(magic, i + 1)
     assert starts, "no offload bundle in .hip_fatbin"
-    notes = []
+    cos = []
     for n, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
         part = tmp_path / f"part{n}.bin"
         part.write_bytes(data[a:b])
@@ -65,9 +65,14 @@ def _notes(tmp_path):
         subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}",
                         f"--output={co}", "--unbundle"], check=True)
-        notes.append(subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
-                                    capture_output=True, text=True, check=True).stdout)
-    return "\n".join(notes)
+        cos.append(co)
+    return cos
+
+
+def _notes(tmp_path):
+    return "\n".join(subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
+                                    capture_output=True, text=True, check=True).stdout
+                     for co in _code_objects(tmp_path))
 
 
 def _kernels(txt):
@@ -103,3 +108,47 @@ def test_kernel_register_budgets(tmp_path):
                          r"rows_kernelILi2ELi20ELi[67]ELb0ELb1ELi1024E")
     spills = {s: v for s, v in ks.items() if v["scratch"] and not ab_only.search(s)}
     assert not spills, list(spills)[:5]
+
+
+def test_persistent_slot_reset_order(tmp_path):
+    """The persistent staged Reconst kernel hands its counter slot back with
+    no fence (kernels.hip, staged_wsp_kernel): the last block swaps both
+    counters to 0 and then clears the slot's pinned host busy word with a
+    relaxed system-scope store.  The order is only right if both swaps have
+    returned (been performed at L2) before that store issues; otherwise the
+    host could give the slot to the next launch while its counters still
+    hold this launch's values, and that launch would skip tiles (wrong
+    Reconst output, xrs.go:236-320).  Pin it in the shipped code object:
+    two returning global_atomic_swap, then s_waitcnt vmcnt(0), then the
+    sc0 sc1 (system-scope) global_store_dword, with no other memory
+    instruction in between."""
+    objdump = os.path.join(LLVM, "llvm-objdump")
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    pat = re.compile(r"_Z\S*staged_wsp_kernelILi12ELi14ELi2ELi2ELi512EE\S*")
+    checked = 0
+    for co in _code_objects(tmp_path):
+        syms = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "-s", "--wide", str(co)],
+                              capture_output=True, text=True, check=True).stdout
+        names = sorted({m.group(0) for m in pat.finditer(syms)
+                        if "." not in m.group(0)})
+        for sym in names:
+            dis = subprocess.run([objdump, "-d", f"--disassemble-symbols={sym}", str(co)],
+                                 capture_output=True, text=True, check=True).stdout
+            ins = [ln.split("//")[0].strip() for ln in dis.splitlines()]
+            ins = [i for i in ins if i and not i.endswith(">:") and not i.startswith("Disassembly")]
+            swaps = [n for n, i in enumerate(ins) if i.startswith("global_atomic_swap")]
+            assert len(swaps) == 2, (sym, [ins[n] for n in swaps])
+            for n in swaps:  # returning form: sc0 (glc) set
+                assert re.search(r"\bsc0\b", ins[n]), ins[n]
+            a, b = swaps
+            assert all(not ins[n].startswith(("global_", "flat_", "buffer_"))
+                       for n in range(a + 1, b)), ins[a:b + 1]
+            tail = ins[b + 1:]
+            st = next(n for n, i in enumerate(tail) if i.startswith("global_store_dword "))
+            assert re.search(r"\bsc0 sc1\b", tail[st]), tail[st]  # the system-scope busy store
+            between = tail[:st]
+            assert any(re.match(r"s_waitcnt .*vmcnt\(0\)", i) for i in between), between
+            assert not any(i.startswith(("global_", "flat_", "buffer_")) for i in between), between
+            checked += 1
+    assert checked >= 1

@@ -172,3 +172,36 @@ def test_launch_local_sigterm_stops_the_ranks(tmp_path):
             time.sleep(0.1)
         else:
             raise AssertionError(f"rank {pid} still running")
+
+
+def test_bench_multi_gpu_keys_8_ranks(tmp_path):
+    """The keys the driver's 8-GPU bench line must carry, built by bench.py's
+    own split / placement functions (config5_plan, xgmi_need_plan) and the
+    start-up device gather, over 8 gloo ranks on CPU
+    (tests/_bench_plan_worker.py): config 5 as an 8-way split of 65,536
+    stripes (8,192 per GPU, contiguous ranges), one rank_devices entry per
+    rank on distinct GPUs, and xgmi_repair's need-set bytes read from peers
+    (ReconstOne's need set, xrs.go:146-221: 8 S of 9 S per stripe read)."""
+    worker = os.path.join(ROOT, "tests", "_bench_plan_worker.py")
+    rc = xdist.launch_local(8, [sys.executable, worker, str(tmp_path)], timeout=300)
+    assert rc == 0
+    line = json.loads((tmp_path / "line.json").read_text())
+    assert line["n_gpus"] == 8 and line["shared_gpu"] is False
+    assert [d["rank"] for d in line["rank_devices"]] == list(range(8))
+    assert len({d["pci"] for d in line["rank_devices"]}) == 8
+    c5 = line["config5"]
+    assert c5["stripes_total"] == 65536 and c5["stripes_per_rank"] == 8192
+    assert c5["rank_ranges"] == [[8192 * r, 8192] for r in range(8)]
+    xg = line["xgmi_repair"]
+    half, spread = xg["layouts"]["half"], xg["layouts"]["spread"]
+    S = 1 << 20
+    # every layout reads the same need set: 8 S per stripe over 64 stripes
+    assert half["need_set_bytes"] == spread["need_set_bytes"] == 64 * 8 * S
+    assert half["need_set_shards"] == 13  # 11 data + parity 12 + parity bi
+    # "half": odd shards on GPU 1; "spread": shard i on GPU i mod 8 (shards 0
+    # and 8 of the need set stay on GPU 0)
+    assert 0 < half["need_set_bytes_remote"] < half["need_set_bytes"]
+    assert half["gpus_read"] == [0, 1]
+    assert spread["need_set_shards_remote"] == spread["need_set_shards"] - 2
+    assert len(spread["gpus_read"]) == 8
+    assert xg["need_set_bytes_remote"] == half["need_set_bytes_remote"]

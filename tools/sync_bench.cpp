@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <thread>
@@ -278,7 +279,8 @@ int main(int argc, char** argv) {
   // per-stripe xrs_encode / xrs_update on ONE codec (the drop-in call
   // pattern; contended calls go through the codec's auto queue)
   // "...reg": the same on registered (xrs_host_alloc) vects
-  if (argc > 2 && (std::strcmp(argv[2], "syncmtreg") == 0 || std::strcmp(argv[2], "queuereg") == 0)) {
+  if (argc > 2 && (std::strcmp(argv[2], "syncmtreg") == 0 || std::strcmp(argv[2], "queuereg") == 0 ||
+                   std::strcmp(argv[2], "queueasyncreg") == 0)) {
     g_reg = true;
     argv[2][std::strlen(argv[2]) - 3] = 0;
   }
@@ -323,6 +325,96 @@ int main(int argc, char** argv) {
                     gib > 0 ? cpu / gib : 0.0);
         std::fflush(stdout);
       }
+    xrs_free(c);
+    std::fflush(stdout);
+    std::_Exit(0);
+  }
+  // `sync_bench SIZE queueasync WAIT_US WINDOW [THREADS...]`: T threads, each
+  // keeping WINDOW Encode stripes in flight through xrs_queue_submit_encode /
+  // xrs_queue_wait (one cgo call site with k stripes outstanding); a BUSY
+  // submit waits on the thread's oldest ticket first.  "...reg": registered
+  // vects.
+  if (argc > 2 && std::strcmp(argv[2], "queueasync") == 0) {
+    const int wait_us = argc > 3 ? std::atoi(argv[3]) : 50;
+    const int window = argc > 4 ? std::max(1, std::atoi(argv[4])) : 8;
+    std::vector<int> tlist = {1, 8, 32};
+    if (argc > 5) {
+      tlist.clear();
+      for (int i = 5; i < argc; ++i) tlist.push_back(std::atoi(argv[i]));
+    }
+    const char* mb = std::getenv("XRS_BENCH_MAX_BATCH");
+    const size_t max_batch = mb && *mb ? std::strtoull(mb, nullptr, 0) : 1024;
+    for (int threads : tlist) {
+      xrs_queue* q = nullptr;
+      if (int e = xrs_queue_new(c, size, max_batch, wait_us, &q)) {
+        std::printf("xrs_queue_new failed: %d\n", e);
+        std::fflush(stdout);
+        return 4;
+      }
+      std::atomic<long> total{0}, busy{0};
+      std::atomic<bool> stop{false};
+      std::vector<std::thread> th;
+      for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+          std::vector<std::unique_ptr<Bufs>> bufs;
+          for (int w = 0; w < window; ++w) bufs.emplace_back(new Bufs(16, size, static_cast<uint8_t>(t + w)));
+          std::vector<xrs_queue_ticket*> live(window, nullptr);  // ring, oldest at head
+          int head = 0, n_live = 0;
+          long n = 0, nb = 0;
+          auto wait_oldest = [&] {
+            if (int rc = xrs_queue_wait(live[head])) {
+              std::printf("xrs_queue_wait failed: %d\n", rc);
+              std::fflush(stdout);
+              std::_Exit(5);
+            }
+            live[head] = nullptr;
+            head = (head + 1) % window;
+            --n_live;
+            ++n;
+          };
+          while (!stop.load(std::memory_order_relaxed)) {
+            if (n_live == window) wait_oldest();
+            const int slot = (head + n_live) % window;
+            xrs_queue_ticket* tk = nullptr;
+            const int rc = xrs_queue_submit_encode(q, bufs[slot]->p.data(), 16, &tk);
+            if (rc == XRS_ERR_BUSY) {
+              ++nb;
+              if (n_live) wait_oldest();
+              else std::this_thread::yield();
+              continue;
+            }
+            if (rc) {
+              std::printf("xrs_queue_submit_encode failed: %d\n", rc);
+              std::fflush(stdout);
+              std::_Exit(5);
+            }
+            live[slot] = tk;
+            ++n_live;
+          }
+          while (n_live) wait_oldest();
+          total += n;
+          busy += nb;
+        });
+      const double t0 = now(), c0 = cpu_now();
+      std::this_thread::sleep_for(std::chrono::seconds(seconds));
+      stop = true;
+      for (auto& x : th) x.join();
+      const double dt = now() - t0, cpu = cpu_now() - c0;
+      const double gib = total * 16.0 * size / (1 << 30);
+      uint64_t st[4] = {0, 0, 0, 0};
+      xrs_queue_stats(q, st);
+      const double nbt = st[0] ? static_cast<double>(st[0]) : 1.0;
+      std::printf("{\"api\": \"xrs_queue_submit_encode + xrs_queue_wait\", \"vect_bytes\": %zu, "
+                  "\"threads\": %d, \"window\": %d, \"registered\": %s, \"stripes_per_s\": %.0f, "
+                  "\"gibps\": %.3f, \"batches\": %llu, \"stripes_per_batch\": %.1f, "
+                  "\"run_us_per_batch\": %.1f, \"wait_us_per_batch\": %.1f, \"busy_returns\": %ld, "
+                  "\"cpu_cores\": %.2f, \"cpu_seconds_per_gib\": %.3f}\n",
+                  size, threads, window, g_reg ? "true" : "false", total / dt, gib / dt,
+                  (unsigned long long)st[0], st[1] / nbt, st[2] / nbt / 1e3, st[3] / nbt / 1e3,
+                  busy.load(), cpu / dt, gib > 0 ? cpu / gib : 0.0);
+      std::fflush(stdout);
+      xrs_queue_free(q);
+    }
     xrs_free(c);
     std::fflush(stdout);
     std::_Exit(0);

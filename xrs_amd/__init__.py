@@ -29,6 +29,7 @@ XRS_ERR_SIZE_NOT_EVEN = -2
 XRS_ERR_ILLEGAL_DATA_INDEX = -3
 XRS_ERR_ILLEGAL_VECTS = -4
 XRS_ERR_INVALID_ARG = -9
+XRS_ERR_BUSY = -11  # xrs_queue_submit_*: no staging batch free (nothing staged)
 
 
 class XRSError(Exception):
@@ -116,6 +117,13 @@ def _load():
         "xrs_queue_update": ([P, P, P, I, PP, I], I),
         "xrs_queue_reconst": ([P, PP, I, IP, I, IP, I], I),
         "xrs_queue_replace": ([P, PP, IP, I, PP, I], I),
+        "xrs_queue_submit_encode": ([P, PP, I, ctypes.POINTER(P)], I),
+        "xrs_queue_submit_reconst_one": ([P, PP, I, I, ctypes.POINTER(P)], I),
+        "xrs_queue_submit_update": ([P, P, P, I, PP, I, ctypes.POINTER(P)], I),
+        "xrs_queue_submit_reconst": ([P, PP, I, IP, I, IP, I, ctypes.POINTER(P)], I),
+        "xrs_queue_submit_replace": ([P, PP, IP, I, PP, I, ctypes.POINTER(P)], I),
+        "xrs_queue_poll": ([P], I),
+        "xrs_queue_wait": ([P], I),
         "xrs_queue_batch_stripes": ([P], Z),
         "xrs_queue_stats": ([P, ctypes.POINTER(ctypes.c_uint64)], I),
         "xrs_queue_batch_sizes": ([P, ctypes.POINTER(ctypes.c_uint64), I], I),
@@ -594,6 +602,55 @@ class XRSQueue:
         _raise(self._call(_lib.xrs_queue_update, _ptr(old_data), _ptr(new_data), int(row),
                           _ptrs(parity), len(parity)), row)
 
+    # ---- asynchronous forms (xrs_queue_submit_* / xrs_queue_wait) ----------
+    def _submit(self, fn, keep, arg, *args):
+        """Stage one call; a QueueTicket, or None when no staging batch is
+        free (XRS_ERR_BUSY: nothing staged, wait on a ticket and resubmit)."""
+        with self._cv:
+            h = self._h
+            if h is None:
+                _raise(XRS_ERR_INVALID_ARG)
+            self._inflight += 1  # until the ticket is waited on (close() waits)
+        t = ctypes.c_void_p()
+        rc = fn(h, *args, ctypes.byref(t))
+        if rc != 0:
+            self._done()
+            if rc == XRS_ERR_BUSY:
+                return None
+            _raise(rc, arg)
+        return QueueTicket(self, t, keep, arg)
+
+    def _done(self):
+        with self._cv:
+            self._inflight -= 1
+            self._cv.notify_all()
+
+    def submit_encode(self, vects):
+        _check_lens(self.size, vects, exact=True)
+        return self._submit(_lib.xrs_queue_submit_encode, vects, self.size, _ptrs(vects), len(vects))
+
+    def submit_reconst_one(self, vects, need_reconst: int):
+        _check_lens(self.size, vects, exact=True)
+        return self._submit(_lib.xrs_queue_submit_reconst_one, vects, need_reconst, _ptrs(vects),
+                            len(vects), int(need_reconst))
+
+    def submit_reconst(self, vects, dp_has, need_reconst):
+        _check_lens(self.size, vects, exact=True)
+        arg = need_reconst[0] if need_reconst else 0
+        return self._submit(_lib.xrs_queue_submit_reconst, vects, arg, _ptrs(vects), len(vects),
+                            _ints(dp_has), len(dp_has), _ints(need_reconst), len(need_reconst))
+
+    def submit_replace(self, data, replace_rows, parity):
+        _check_lens(self.size, data, parity, exact=True)
+        bad = next((r for r in replace_rows if r < 0 or r >= self._codec.data_num), 0)
+        return self._submit(_lib.xrs_queue_submit_replace, (data, parity), bad, _ptrs(data),
+                            _ints(replace_rows), len(replace_rows), _ptrs(parity), len(parity))
+
+    def submit_update(self, old_data, new_data, row: int, parity):
+        _check_lens(self.size, [old_data, new_data], parity, exact=True)
+        return self._submit(_lib.xrs_queue_submit_update, (old_data, new_data, parity), row,
+                            _ptr(old_data), _ptr(new_data), int(row), _ptrs(parity), len(parity))
+
     def stats(self) -> dict:
         """Batches and stripes run so far, and summed device / queueing ns."""
         out = (ctypes.c_uint64 * 4)()
@@ -614,3 +671,34 @@ class XRSQueue:
         buf = ctypes.create_string_buffer(n + 1)
         _lib.xrs_queue_dump(self._h, buf, n + 1)
         return buf.value.decode()
+
+
+class QueueTicket:
+    """One staged asynchronous call (XRSQueue.submit_*): wait() blocks until
+    its stripe is done, copies the outputs back and raises the call's error;
+    done() polls.  Holds the call's buffers until waited on; every ticket is
+    waited on once (an abandoned ticket is waited on when collected)."""
+
+    def __init__(self, q: XRSQueue, handle, keep, arg):
+        self._q, self._t, self._keep, self._arg = q, handle, keep, arg
+
+    def done(self) -> bool:
+        return self._t is None or _lib.xrs_queue_poll(self._t) == 1
+
+    def wait(self) -> None:
+        t, self._t = self._t, None
+        if t is None:
+            return
+        try:
+            rc = _lib.xrs_queue_wait(t)
+        finally:
+            self._keep = None
+            self._q._done()
+        _raise(rc, self._arg)
+
+    def __del__(self):
+        if self._t is not None:
+            try:
+                self.wait()
+            except XRSError:
+                pass

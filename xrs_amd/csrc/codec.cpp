@@ -1035,6 +1035,7 @@ const char* xrs_strerror(int code) {
     case XRS_ERR_HIP: return "hip runtime error";
     case XRS_ERR_INVALID_ARG: return "invalid argument";
     case XRS_ERR_NO_DEVICE: return "no gpu device";
+    case XRS_ERR_BUSY: return "queue busy";
     default: return "unknown error";
   }
 }

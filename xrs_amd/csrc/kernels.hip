@@ -919,13 +919,21 @@ __global__ __launch_bounds__(2 * T) void staged_wsp_kernel(const StagedArgs<NL, 
     // atomic has returned (the loop exit reads its value) before its arrival
     // is issued, so every tile atomic of the launch is performed before the
     // last arrival; the resets are exchanges whose returned values the busy
-    // store waits for, so they are performed before the host sees the slot
-    // free.
+    // store's value depends on, so they are performed before the host sees
+    // the slot free.  The dependency is one the compiler cannot fold: ctr[1]
+    // returns gridDim.x (< 2^31), so (r0 & r1) == ~0u is false and the store
+    // writes 0, but only the returned values say so; the explicit vmcnt(0)
+    // wait (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15) states the order
+    // in the code object as well.  tests/test_kernel_resources.py
+    // (test_persistent_slot_reset_order) checks the disassembly: both
+    // returning swaps, then s_waitcnt vmcnt(0), then the busy store.
     if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - 1) {
-      uint32_t r0 = __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t r1 = __hip_atomic_exchange(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" : "+v"(r0), "+v"(r1));  // both returns consumed before the store below
-      __hip_atomic_store(busy, (r0 & r1) & 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t r0 = __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t r1 =
+          __hip_atomic_exchange(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __hip_atomic_store(busy, (r0 & r1) == ~0u ? 1u : 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }

@@ -213,9 +213,56 @@ struct xrs_queue {
       if (stop) cv_free.notify_all();
     }
   }
+  // A staged call: its batch, slot and the batch's completion count when it
+  // was reserved, and the pieces to copy back after the batch ran.
+  struct Staged {
+    Batch* bt = nullptr;
+    size_t slot = 0;
+    uint32_t seq = 0;
+    bool reg = false;  // the call's vects are registered: no copies
+    std::vector<Piece> out;
+  };
+  // Reserve a slot and stage the call (no wait).  nonblock: XRS_ERR_BUSY
+  // instead of waiting for a free staging batch.
+  int stage(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
+            const std::vector<int>* has, const std::vector<int>* need, bool nonblock, Staged* sc);
+  // Wait for a staged call's batch, copy its outputs back, release the slot.
+  int wait(Staged& sc);
   int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1,
-             const std::vector<int>* has = nullptr, const std::vector<int>* need = nullptr);
+             const std::vector<int>* has = nullptr, const std::vector<int>* need = nullptr) {
+    Staged sc;
+    const int e = stage(key, in, out, row, has, need, false, &sc);
+    return e ? e : wait(sc);
+  }
+  // The synchronous call (t == nullptr) or its asynchronous form (*t: a
+  // ticket for xrs_queue_wait).
+  int run(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
+          const std::vector<int>* has, const std::vector<int>* need, xrs_queue_ticket** t);
 };
+
+// An asynchronous call (xrs_queue_submit_*): staged in a batch, or already
+// finished (st.bt == nullptr: a call the queue ran directly, status `err`).
+struct xrs_queue_ticket {
+  xrs_queue* q = nullptr;
+  xrs_queue::Staged st;
+  int err = 0;
+};
+
+int xrs_queue::run(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
+                   const std::vector<int>* has, const std::vector<int>* need,
+                   xrs_queue_ticket** t) {
+  if (!t) return submit(key, in, out, row, has, need);
+  *t = nullptr;
+  auto* tk = new xrs_queue_ticket();
+  tk->q = this;
+  const int e = stage(key, in, out, row, has, need, true, &tk->st);
+  if (e) {
+    delete tk;
+    return e;
+  }
+  *t = tk;
+  return XRS_OK;
+}
 
 // Enqueue batch bt on its stream, ending with the write of its sequence
 // number to its host word.  Returns an XRS error if anything failed to
@@ -428,8 +475,9 @@ void xrs_queue::complete() {
   }
 }
 
-int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out,
-                      int row, const std::vector<int>* has, const std::vector<int>* need) {
+int xrs_queue::stage(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
+                     const std::vector<int>* has, const std::vector<int>* need, bool nonblock,
+                     Staged* sc) {
   auto same_pattern = [&](const Batch& bt) {
     return !has || (bt.pat_has == *has && bt.pat_need == *need);
   };
@@ -467,6 +515,11 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
       for (int i = 0; i < n_batches && f < 0; ++i)
         if (b[i].state == FREE) f = i;
       if (f < 0) {
+        if (nonblock) {  // (xrs_queue_submit_*: the caller waits on a ticket first)
+          lk.unlock();
+          leave();
+          return XRS_ERR_BUSY;
+        }
         cv_free.wait(lk);
         continue;
       }
@@ -514,6 +567,20 @@ int xrs_queue::submit(int key, const std::vector<Piece>& in, const std::vector<P
     std::lock_guard<std::mutex> lk(mu);
     cv_work.notify_one();
   }
+  sc->bt = &bt;
+  sc->slot = slot;
+  sc->seq = seq;
+  sc->reg = reg;
+  sc->out = out;
+  return XRS_OK;
+}
+
+int xrs_queue::wait(Staged& sc) {
+  Batch& bt = *sc.bt;
+  const uint32_t seq = sc.seq;
+  const bool reg = sc.reg;
+  const std::vector<Piece>& out = sc.out;
+  uint8_t* st = bt.host + bo + sc.slot * stripe_bytes;
   while (bt.done.load(std::memory_order_acquire) == seq) futex_wait(&bt.done, seq);
   // The batch cannot be recycled before this caller's own release below, so
   // its slot count and status are read here, once: after the release another
@@ -660,7 +727,7 @@ void xrs_queue_free(xrs_queue* q) {
 
 // xrs.go:103 Encode, coalesced with concurrent callers: data rows in,
 // parity rows out.
-int xrs_queue_encode(xrs_queue* q, uint8_t* const* vects, int n) {
+static int queue_encode(xrs_queue* q, uint8_t* const* vects, int n, xrs_queue_ticket** t) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (!vects || n != q->d + q->p) return XRS_ERR_ILLEGAL_VECTS;
   for (int i = 0; i < n; ++i)
@@ -668,13 +735,13 @@ int xrs_queue_encode(xrs_queue* q, uint8_t* const* vects, int n) {
   std::vector<xrs_queue::Piece> in, out;
   for (int j = 0; j < q->d; ++j) in.push_back({vects[j], j, 0, q->size});
   for (int r = 0; r < q->p; ++r) out.push_back({vects[q->d + r], q->d + r, 0, q->size});
-  return q->submit(0, in, out);
+  return q->run(0, in, out, -1, nullptr, nullptr, t);
 }
 
 // xrs.go:175 ReconstOne, coalesced: only the GetNeedVects set is copied in
 // (b-halves of the d survivors and of parity bi, a-halves of aNeed), vect k
 // out.
-int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
+static int queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k, xrs_queue_ticket** t) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (k < 0 || k >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
   if (!vects || n != q->d + q->p) return XRS_ERR_ILLEGAL_VECTS;
@@ -693,14 +760,14 @@ int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
   in.push_back({vects[bi], bi, half, half});
   for (int a : a_need) in.push_back({vects[a], a, 0, half});
   out.push_back({vects[k], k, 0, q->size});
-  return q->submit(1 + k, in, out);
+  return q->run(1 + k, in, out, -1, nullptr, nullptr, t);
 }
 
 // xrs.go:324 Update(oldData, newData, row, parity), coalesced across rows
 // (each staged stripe carries its own row: update_rows kernel): staged rows
 // [0, p) parity, p old, p+1 new; parity out.
-int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_data, int row,
-                     uint8_t* const* parity, int n_parity) {
+static int queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_data, int row,
+                         uint8_t* const* parity, int n_parity, xrs_queue_ticket** t) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (row < 0 || row >= q->d) return XRS_ERR_ILLEGAL_DATA_INDEX;
   if (!parity || n_parity != q->p) return XRS_ERR_ILLEGAL_VECTS;
@@ -714,7 +781,7 @@ int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_d
   }
   in.push_back({const_cast<uint8_t*>(old_data), q->p, 0, q->size});
   in.push_back({const_cast<uint8_t*>(new_data), q->p + 1, 0, q->size});
-  return q->submit(1 + q->d, in, out, row);
+  return q->run(1 + q->d, in, out, row, nullptr, nullptr, t);
 }
 
 // xrs.go:236 Reconst(vects, dpHas, needReconst), coalesced: calls with the
@@ -724,13 +791,13 @@ int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_d
 // xrs.go:305-320) and of every needed vect.  A call whose indexes are not all
 // valid and distinct, or whose need overlaps dpHas, runs as a plain
 // xrs_reconst (the reference's partial side effects and toggling).
-int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_has, int n_has,
-                      const int* need, int n_need) {
+static int queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_has, int n_has,
+                          const int* need, int n_need, xrs_queue_ticket** t) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (n_has < 0 || n_need < 0 || (n_has && !dp_has) || (n_need && !need))
     return XRS_ERR_INVALID_ARG;
   if (n_need == 1 && need[0] < q->d)  // xrs.go:238-240 (a negative k is rejected there)
-    return xrs_queue_reconst_one(q, vects, n, need[0]);
+    return queue_reconst_one(q, vects, n, need[0], t);
   const int d = q->d, m = q->d + q->p;
   if (!vects || n != m) return XRS_ERR_ILLEGAL_VECTS;
   for (int i = 0; i < n; ++i)
@@ -745,8 +812,14 @@ int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_
     clean = need[u] >= 0 && need[u] < m && !in_has[need[u]] && !in_need[need[u]];
     if (clean) in_need[need[u]] = 1;
   }
-  if (!clean)
-    return xrs_detail::reconst_direct(q->codec, vects, n, q->size, dp_has, n_has, need, n_need);
+  if (!clean) {  // runs now; an asynchronous caller gets a finished ticket
+    const int e = xrs_detail::reconst_direct(q->codec, vects, n, q->size, dp_has, n_has, need, n_need);
+    if (!t) return e;
+    *t = new xrs_queue_ticket();
+    (*t)->q = q;
+    (*t)->err = e;
+    return XRS_OK;
+  }
   const size_t half = q->size / 2;
   std::vector<xrs_queue::Piece> in, out;
   for (int i = 0; i < m; ++i) {
@@ -761,14 +834,14 @@ int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_
     }
   }
   const std::vector<int> has(dp_has, dp_has + n_has), nd(need, need + n_need);
-  return q->submit(2 + d, in, out, -1, &has, &nd);
+  return q->run(2 + d, in, out, -1, &has, &nd, t);
 }
 
 // xrs.go:363 Replace(data, replaceRows, parity), coalesced: calls with the
 // same rows share a batch (staged rows [0, p) parity, [p, p+n) data);
 // parity out.
-int xrs_queue_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n,
-                      uint8_t* const* parity, int n_parity) {
+static int queue_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n,
+                          uint8_t* const* parity, int n_parity, xrs_queue_ticket** t) {
   if (!q) return XRS_ERR_INVALID_ARG;
   if (n < 1 || n > q->d) return XRS_ERR_ILLEGAL_VECTS;
   if (!rows) return XRS_ERR_INVALID_ARG;
@@ -787,7 +860,68 @@ int xrs_queue_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n
   }
   for (int i = 0; i < n; ++i) in.push_back({data[i], q->p + i, 0, q->size});
   const std::vector<int> rv(rows, rows + n), none;
-  return q->submit(3 + q->d, in, out, -1, &rv, &none);
+  return q->run(3 + q->d, in, out, -1, &rv, &none, t);
+}
+
+int xrs_queue_encode(xrs_queue* q, uint8_t* const* vects, int n) {
+  return queue_encode(q, vects, n, nullptr);
+}
+int xrs_queue_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k) {
+  return queue_reconst_one(q, vects, n, k, nullptr);
+}
+int xrs_queue_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_data, int row,
+                     uint8_t* const* parity, int n_parity) {
+  return queue_update(q, old_data, new_data, row, parity, n_parity, nullptr);
+}
+int xrs_queue_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_has, int n_has,
+                      const int* need, int n_need) {
+  return queue_reconst(q, vects, n, dp_has, n_has, need, n_need, nullptr);
+}
+int xrs_queue_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n,
+                      uint8_t* const* parity, int n_parity) {
+  return queue_replace(q, data, rows, n, parity, n_parity, nullptr);
+}
+
+// ---- asynchronous forms: stage now, xrs_queue_wait later ----------------
+// A submit that finds no free staging batch returns XRS_ERR_BUSY with nothing
+// staged (a blocking wait there could deadlock a thread whose own tickets
+// hold every batch); the caller waits on one of its tickets and submits again.
+#define XRS_SUBMIT(call)             \
+  if (!t) return XRS_ERR_INVALID_ARG; \
+  *t = nullptr;                      \
+  return call
+int xrs_queue_submit_encode(xrs_queue* q, uint8_t* const* vects, int n, xrs_queue_ticket** t) {
+  XRS_SUBMIT(queue_encode(q, vects, n, t));
+}
+int xrs_queue_submit_reconst_one(xrs_queue* q, uint8_t* const* vects, int n, int k,
+                                 xrs_queue_ticket** t) {
+  XRS_SUBMIT(queue_reconst_one(q, vects, n, k, t));
+}
+int xrs_queue_submit_update(xrs_queue* q, const uint8_t* old_data, const uint8_t* new_data,
+                            int row, uint8_t* const* parity, int n_parity, xrs_queue_ticket** t) {
+  XRS_SUBMIT(queue_update(q, old_data, new_data, row, parity, n_parity, t));
+}
+int xrs_queue_submit_reconst(xrs_queue* q, uint8_t* const* vects, int n, const int* dp_has,
+                             int n_has, const int* need, int n_need, xrs_queue_ticket** t) {
+  XRS_SUBMIT(queue_reconst(q, vects, n, dp_has, n_has, need, n_need, t));
+}
+int xrs_queue_submit_replace(xrs_queue* q, uint8_t* const* data, const int* rows, int n,
+                             uint8_t* const* parity, int n_parity, xrs_queue_ticket** t) {
+  XRS_SUBMIT(queue_replace(q, data, rows, n, parity, n_parity, t));
+}
+#undef XRS_SUBMIT
+
+int xrs_queue_poll(const xrs_queue_ticket* t) {
+  if (!t) return XRS_ERR_INVALID_ARG;
+  if (!t->st.bt) return 1;
+  return t->st.bt->done.load(std::memory_order_acquire) != t->st.seq ? 1 : 0;
+}
+
+int xrs_queue_wait(xrs_queue_ticket* t) {
+  if (!t) return XRS_ERR_INVALID_ARG;
+  const int e = t->st.bt ? t->q->wait(t->st) : t->err;
+  delete t;
+  return e;
 }
 
 size_t xrs_queue_batch_stripes(const xrs_queue* q) { return q ? q->max_batch : 0; }

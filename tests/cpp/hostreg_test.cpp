@@ -1,9 +1,11 @@
 // hostreg_test.cpp -- CPU test of the registered-range table
 // (xrs_amd/csrc/hostreg.cpp, compiled alone: no HIP): lookups at range edges,
 // replacement, and readers racing a writer that registers and unregisters,
-// with every replaced table freed once no reader holds it.  Built twice, under
+// with every replaced table freed by the writer once no reader can hold it (a
+// two-generation grace period; a writer waits for a view held across it).  Built twice, under
 // ThreadSanitizer and under AddressSanitizer (tests/test_cpp.py).
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
@@ -26,7 +28,8 @@ static uint64_t dev_of(const void* p, size_t n) {
   return v.device(p, n);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int replacements = argc > 1 ? std::atoi(argv[1]) : 20000;
   static char a[4096], b[4096];
   CHECK(dev_of(a, 1) == 0);
   xrs_detail::host_ranges_add(a, sizeof a, reinterpret_cast<void*>(0x100000));
@@ -44,6 +47,27 @@ int main() {
   CHECK(dev_of(b, 1) == 0xA00000);
   xrs_detail::host_ranges_remove(a);  // absent: no-op
   CHECK(xrs_detail::host_ranges_retired() == 0);  // no reader: freed at once
+
+  // a view held across a replacement: the writer waits for it, and the view's
+  // table stays readable until it is dropped (ASan: no use after free)
+  {
+    std::atomic<bool> wrote{false};
+    std::thread w;
+    {
+      const HostRangesView held;
+      w = std::thread([&] {
+        xrs_detail::host_ranges_add(a, 8, reinterpret_cast<void*>(0x300000));
+        wrote = true;
+      });
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      CHECK(!wrote.load());                      // blocked on the held view
+      CHECK(held.device(b + 4, 4) == 0xA00000 + 4);  // the old table, intact
+      CHECK(held.device(a, 1) == 0);             // a was removed in that table
+    }
+    w.join();
+    CHECK(wrote.load() && dev_of(a, 8) == 0x300000);
+    xrs_detail::host_ranges_remove(a);
+  }
 
   // readers race a writer flipping 64 ranges; a reader must always see either
   // nothing or the right address for a flipping range, and b throughout
@@ -66,18 +90,18 @@ int main() {
         lookups.fetch_add(16, std::memory_order_relaxed);
       }
     });
-  for (int round = 0; round < 20000; ++round) {
+  for (int round = 0; round < replacements; ++round) {
     const int i = round % 64;
     if ((round / 64) % 2 == 0)
       xrs_detail::host_ranges_add(pool[i], sizeof pool[i], reinterpret_cast<void*>(0x10000000ull * (i + 1)));
     else
       xrs_detail::host_ranges_remove(pool[i]);
+    CHECK(xrs_detail::host_ranges_retired() == 0);  // freed by the writer, under load
   }
   stop = true;
   for (auto& x : th) x.join();
-  // quiescent now: the next replacement frees every retired table
   xrs_detail::host_ranges_add(a, 16, reinterpret_cast<void*>(0x100000));
   CHECK(xrs_detail::host_ranges_retired() == 0);
-  std::printf("PASS hostreg: %ld lookups against 20000 replacements\n", lookups.load());
+  std::printf("PASS hostreg: %ld lookups against %d replacements\n", lookups.load(), replacements);
   return 0;
 }

@@ -6,6 +6,7 @@ Every result is compared with the oracle (oracle/xrs_oracle.c).  Reference
 semantics: xrs.go:103-128 (Encode), :175-221 (ReconstOne), :236-320
 (Reconst), :324-346 (Update), :363-387 (Replace); the size rule is
 xrs.go:130-136 (any even size)."""
+import ctypes
 import threading
 
 import numpy as np
@@ -177,3 +178,115 @@ def test_host_pipeline_odd_sizes(rng, size, n):
     x.replace_host(dbuf.ctypes.data, size, 3 * size, rows, size, buf.ctypes.data + D * size, size,
                    stripe, n)
     assert np.array_equal(v, exp)
+
+
+# (vect size, base offset, shard pad, stripe pad): host layouts whose rows sit
+# on every address residue mod 4 and whose pitches are not multiples of 4, so
+# the pipeline's device image is residue-matched and its copies split into
+# pitch groups (codec.cpp copy_rows / plan_image)
+ANY_LAYOUTS = [(4098, 0, 0, 0), (4098, 1, 0, 1), (4100, 2, 3, 2), (4100, 3, 5, 3),
+               (1026, 1, 1, 0), (1026, 2, 2, 6), (4096, 1, 0, 0), (4096, 0, 2, 2),
+               ((1 << 20) + 2, 3, 1, 1), (2, 1, 1, 1)]
+
+
+@pytest.mark.parametrize("mode", ["pageable", "pinned_dma"])
+@pytest.mark.parametrize("size,base_off,shard_pad,stripe_pad", ANY_LAYOUTS)
+def test_host_pipeline_any_layout(rng, monkeypatch, size, base_off, shard_pad, stripe_pad, mode):
+    """The host copy pipeline on any host layout (xrs_*_host through the
+    device slots: pageable memory, or pinned with XRS_HOST_ZC=0): Encode,
+    ReconstOne, Reconst (2 lost, retrieveRS side effect), Update from a
+    separate odd-strided buffer and Replace(2), every vect vs the oracle and
+    every byte outside the vects the call writes unchanged (no widened copy
+    writes host memory).  Reference semantics: xrs.go:103-387."""
+    if mode == "pinned_dma":
+        monkeypatch.setenv("XRS_HOST_ZC", "0")
+    o, x, L = OracleXRS(D, P), xrs_amd.XRS(D, P), xrs_amd.lib()
+    n = 3 if size > (1 << 16) else 150
+    shard, stripe = size + shard_pad, 16 * (size + shard_pad) + stripe_pad
+    total = base_off + n * stripe + 64
+    pins = []
+
+    def host(nbytes):
+        if mode == "pageable":
+            a = np.empty(nbytes, np.uint8)
+            return a.ctypes.data, a
+        p = L.xrs_host_alloc(nbytes)
+        assert p
+        pins.append(p)
+        return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+    try:
+        ptr, buf = host(total)
+        buf[:] = rng.integers(0, 256, size=total, dtype=np.uint8)
+        base = ptr + base_off
+
+        def at(s, i):
+            a = base_off + s * stripe + i * shard
+            return slice(a, a + size)
+
+        def vects(b, s):
+            return [b[at(s, i)].copy() for i in range(D + P)]
+
+        def check(want, written, what):
+            for s in range(n):
+                for i in range(D + P):
+                    assert np.array_equal(buf[at(s, i)], want[s][i]), (what, s, i)
+            mask = np.ones(total, bool)
+            for s in range(n):
+                for i in written:
+                    mask[at(s, i)] = False
+            assert np.array_equal(buf[mask], before[mask]), (what, "bytes outside the written vects")
+
+        # Encode
+        before = buf.copy()
+        want = [vects(buf, s) for s in range(n)]
+        for w in want:
+            o.encode(w)
+        x.encode_host(base, size, shard, stripe, n)
+        check(want, range(D, D + P), "encode")
+        # ReconstOne(k): vect k zeroed first
+        k = 7
+        for s in range(n):
+            buf[at(s, k)] = 0
+        before = buf.copy()
+        x.reconst_one_host(base, size, shard, stripe, n, k)
+        check(want, [k], "reconst_one")
+        # Reconst of data 2 and parity 13, both needed
+        lost = [2, 13]
+        has = [j for j in range(D + P) if j not in lost]
+        for s in range(n):
+            for j in lost:
+                buf[at(s, j)] = 0x5A
+        before = buf.copy()
+        want = [vects(buf, s) for s in range(n)]
+        for w in want:
+            o.reconst(w, has, lost)
+        x.reconst_host(base, size, shard, stripe, n, has, lost)
+        check(want, range(D + P), "reconst")
+        # Update(row) with new data from a separate buffer, odd stride
+        row, nstride = 4, size + 3
+        nptr, nbuf = host(1 + n * nstride + 8)
+        nbuf[:] = rng.integers(0, 256, size=len(nbuf), dtype=np.uint8)
+        before = buf.copy()
+        want = [vects(buf, s) for s in range(n)]
+        for s in range(n):
+            new = nbuf[1 + s * nstride:1 + s * nstride + size]
+            o.update(want[s][row].copy(), new, row, want[s][D:])
+        x.update_host(base + row * shard, stripe, nptr + 1, nstride, size, row,
+                      base + D * shard, shard, stripe, n)
+        check(want, range(D, D + P), "update")
+        # Replace(rows 1, 10) with data from that buffer: 2 vects per stripe
+        rows = [1, 10]
+        dshard, dstride = size + 1, 2 * (size + 1) + 2
+        dptr, dbuf = host(3 + n * dstride + 8)
+        dbuf[:] = rng.integers(0, 256, size=len(dbuf), dtype=np.uint8)
+        before = buf.copy()
+        want = [vects(buf, s) for s in range(n)]
+        for s in range(n):
+            data = [dbuf[3 + s * dstride + i * dshard:][:size] for i in range(2)]
+            o.replace(data, rows, want[s][D:])
+        x.replace_host(dptr + 3, dshard, dstride, rows, size, base + D * shard, shard, stripe, n)
+        check(want, range(D, D + P), "replace")
+    finally:
+        for p in pins:
+            L.xrs_host_free(p)

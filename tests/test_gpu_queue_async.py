@@ -33,9 +33,18 @@ def test_async_one_thread_every_op(size):
     rng = np.random.Generator(np.random.PCG64(size))
     n = 24 if size < (1 << 20) else 6
 
-    def run(tickets):
-        for t in tickets:
-            assert t is not None
+    def run(submits):
+        """Submit every call, waiting on the oldest ticket whenever the queue
+        says busy (calls of different keys, e.g. ReconstOne of different k,
+        each open a batch), then wait on the rest."""
+        live = []
+        for sub in submits:
+            t = sub()
+            while t is None:
+                live.pop(0).wait()
+                t = sub()
+            live.append(t)
+        for t in live:
             t.wait()
 
     stripes = [[rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(D + P)]
@@ -43,7 +52,7 @@ def test_async_one_thread_every_op(size):
     refs = [[a.copy() for a in v] for v in stripes]
     for r in refs:
         o.encode(r)
-    run([q.submit_encode(v) for v in stripes])
+    run([lambda v=v: q.submit_encode(v) for v in stripes])
     assert all(_same(v, r) for v, r in zip(stripes, refs)), "encode"
     # ReconstOne(k), k per stripe
     ks = [int(rng.integers(0, D)) for _ in range(n)]
@@ -53,7 +62,7 @@ def test_async_one_thread_every_op(size):
         for j in range(D + P):
             if j not in a_need and j != k:
                 v[j][: size // 2] = 0xC3
-    run([q.submit_reconst_one(v, k) for v, k in zip(stripes, ks)])
+    run([lambda v=v, k=k: q.submit_reconst_one(v, k) for v, k in zip(stripes, ks)])
     assert all(np.array_equal(v[k], r[k]) for v, r, k in zip(stripes, refs, ks)), "reconst_one"
     for v, r in zip(stripes, refs):
         for j in range(D + P):
@@ -61,7 +70,8 @@ def test_async_one_thread_every_op(size):
     # Update(row) with fresh data
     news = [rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(n)]
     rows = [int(rng.integers(0, D)) for _ in range(n)]
-    run([q.submit_update(v[row], new, row, v[D:]) for v, new, row in zip(stripes, news, rows)])
+    run([lambda v=v, new=new, row=row: q.submit_update(v[row], new, row, v[D:])
+         for v, new, row in zip(stripes, news, rows)])
     for r, new, row in zip(refs, news, rows):
         o.update(r[row], new, row, r[D:])
         r[row][:] = new
@@ -70,7 +80,7 @@ def test_async_one_thread_every_op(size):
     assert all(_same(v, r) for v, r in zip(stripes, refs)), "update"
     # Replace(rows 1, 7)
     datas = [[rng.integers(0, 256, size=size, dtype=np.uint8) for _ in range(2)] for _ in range(n)]
-    run([q.submit_replace(dd, [1, 7], v[D:]) for v, dd in zip(stripes, datas)])
+    run([lambda v=v, dd=dd: q.submit_replace(dd, [1, 7], v[D:]) for v, dd in zip(stripes, datas)])
     for r, dd in zip(refs, datas):
         o.replace(dd, [1, 7], r[D:])
     assert all(_same(v[D:], r[D:]) for v, r in zip(stripes, refs)), "replace"
@@ -82,7 +92,7 @@ def test_async_one_thread_every_op(size):
             v[j][:] = 0x5A
             r[j][:] = 0x5A
         o.reconst(r, has, lost)
-    run([q.submit_reconst(v, has, lost) for v in stripes])
+    run([lambda v=v: q.submit_reconst(v, has, lost) for v in stripes])
     assert all(_same(v, r) for v, r in zip(stripes, refs)), "reconst"
     # an unclean Reconst (repeated index) runs at once: a finished ticket
     v, r = stripes[0], [a.copy() for a in stripes[0]]

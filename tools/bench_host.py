@@ -128,6 +128,10 @@ def main():
     modes = sys.argv[1:] or ["pipeline", "zero-copy"]
     if "reconst2" in modes:  # only the general-Reconst rows, pipeline modes
         cases, modes = [c for c in cases if c[0] == "reconst_2"], ["pipeline"]
+    if "odd" in modes:  # odd vect sizes (back-to-back shards), pipeline modes
+        cases = [("encode", 4098, 16384), ("encode", 4100, 16384), ("encode", (1 << 20) + 2, 64),
+                 ("reconst_one", 4098, 16384), ("reconst_one", (1 << 20) + 2, 64)]
+        modes = ["pipeline"]
     for op, size, n in cases:
         if "pipeline" in modes:
             for pinned, zc in ((True, "1"), (True, "0"), (False, "0")):

@@ -103,6 +103,7 @@ int main() {
         std::fflush(stderr);
         for (size_t i = 0; i < n; ++i) host[off + i] = static_cast<uint8_t>(i * 29 + off);
         CK(hipMemcpyAsync(dev + off, host + off, n, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));  // (pinned: the DMA reads host memory later)
         std::memset(host, 0, n + 8);
         CK(hipMemcpyAsync(host + off, dev + off, n, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));

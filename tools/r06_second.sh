@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 o=gpurun_out
 step() { echo "== $*"; }
 step pytest && timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-    tests/test_gpu_queue_async.py tests/test_gpu_edge.py tests/test_gpu_shards.py tests/test_cpp.py \
+    -m gpu tests/test_gpu_queue_async.py tests/test_gpu_edge.py tests/test_gpu_shards.py tests/test_cpp.py \
     > $o/r06_pytest_b.log 2>&1 &&
   tail -3 $o/r06_pytest_b.log &&
   step dma probe && AMD_LOG_LEVEL=1 timeout -k 10 180 ./tools/dma_rect_probe > $o/r06_dma_rect_probe.log 2>&1 &&

@@ -35,13 +35,14 @@ static double cpu_now() {
 // allocation the library knows as pinned and mapped, so the per-stripe calls
 // skip the CPU copies through staging (the cgo shim's pinned buffer pool).
 static bool g_reg = false;
+static bool g_mixed = false;  // "queuemixed": odd caller threads registered, even ones plain
 struct Bufs {
   std::vector<std::vector<uint8_t>> own;
   void* pinned = nullptr;
   std::vector<uint8_t*> p;
-  Bufs(int n, size_t size, uint8_t fill) {
+  Bufs(int n, size_t size, uint8_t fill, bool reg = g_reg) {
     const size_t stride = (size + 63) / 64 * 64;
-    if (g_reg) {
+    if (reg) {
       pinned = xrs_host_alloc(stride * n);
       if (!pinned) {
         std::printf("xrs_host_alloc failed\n");
@@ -334,6 +335,10 @@ int main(int argc, char** argv) {
   // xrs_queue_wait (one cgo call site with k stripes outstanding); a BUSY
   // submit waits on the thread's oldest ticket first.  "...reg": registered
   // vects.
+  if (argc > 2 && std::strcmp(argv[2], "queuemixed") == 0) {  // then as "queue"
+    g_mixed = true;
+    argv[2][5] = 0;
+  }
   if (argc > 2 && std::strcmp(argv[2], "queueasync") == 0) {
     const int wait_us = argc > 3 ? std::atoi(argv[3]) : 50;
     const int window = argc > 4 ? std::max(1, std::atoi(argv[4])) : 8;
@@ -377,10 +382,17 @@ int main(int argc, char** argv) {
             const int slot = (head + n_live) % window;
             xrs_queue_ticket* tk = nullptr;
             const int rc = xrs_queue_submit_encode(q, bufs[slot]->p.data(), 16, &tk);
-            if (rc == XRS_ERR_BUSY) {
+            if (rc == XRS_ERR_BUSY) {  // wait on our oldest; with none, the blocking call
               ++nb;
-              if (n_live) wait_oldest();
-              else std::this_thread::yield();
+              if (n_live) {
+                wait_oldest();
+              } else if (int rs = xrs_queue_encode(q, bufs[slot]->p.data(), 16)) {
+                std::printf("xrs_queue_encode failed: %d\n", rs);
+                std::fflush(stdout);
+                std::_Exit(5);
+              } else {
+                ++n;
+              }
               continue;
             }
             if (rc) {
@@ -472,7 +484,7 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
       th.emplace_back([&, t] {
-        Bufs b(16, size, static_cast<uint8_t>(t));
+        Bufs b(16, size, static_cast<uint8_t>(t), g_mixed ? (t % 2 == 1) : g_reg);
         std::vector<uint8_t*>& p = b.p;
         long n = 0;
         while (!stop.load(std::memory_order_relaxed)) {
@@ -517,7 +529,7 @@ int main(int argc, char** argv) {
                 "\"stripes_per_batch\": %.1f, \"run_us_per_batch\": %.1f, "
                 "\"wait_us_per_batch\": %.1f, \"cpu_cores\": %.2f, \"cpu_seconds_per_gib\": %.3f}\n",
                 upd ? "xrs_queue_update" : "xrs_queue_encode",
-                size, threads, g_reg ? "true" : "false", total / dt, gib / dt, (unsigned long long)st[0], st[1] / nb,
+                size, threads, g_mixed ? "\"half\"" : g_reg ? "true" : "false", total / dt, gib / dt, (unsigned long long)st[0], st[1] / nb,
                 st[2] / nb / 1e3, st[3] / nb / 1e3, cpu / dt, gib > 0 ? cpu / gib : 0.0);
     std::fflush(stdout);
     if (std::getenv("XRS_QUEUE_DUMP")) {

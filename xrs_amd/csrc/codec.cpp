@@ -65,6 +65,8 @@ struct xrs_codec {
   mutable uint8_t* slot[kPipe] = {nullptr, nullptr, nullptr};
   mutable size_t slot_cap = 0;
   mutable hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
+  mutable uint8_t* bounce[kPipe] = {nullptr, nullptr, nullptr};  // pinned (HeadBounce)
+  mutable size_t bounce_cap = 0;
 
   uint8_t g(int row, int col) const { return gen[static_cast<size_t>(row) * d + col]; }
 };
@@ -830,7 +832,7 @@ class Stage {
 // ---------------------------------------------------- host-resident pipeline
 constexpr size_t kChunkBytes = 64u << 20;  // device bytes per pipeline chunk
 
-int ensure_pipe(const xrs_codec* x, size_t bytes) {
+int ensure_pipe(const xrs_codec* x, size_t bytes, size_t bounce) {
   if (x->device < 0) return XRS_ERR_NO_DEVICE;
   for (int i = 0; i < xrs_codec::kPipe; ++i)
     if (!x->pstream[i] && hipStreamCreateWithFlags(&x->pstream[i], hipStreamNonBlocking) != hipSuccess)
@@ -845,116 +847,240 @@ int ensure_pipe(const xrs_codec* x, size_t bytes) {
       if (hipMalloc(&x->slot[i], bytes) != hipSuccess) return XRS_ERR_HIP;
     x->slot_cap = bytes;
   }
+  if (bounce > x->bounce_cap) {
+    for (int i = 0; i < xrs_codec::kPipe; ++i) {
+      if (x->bounce[i]) (void)hipHostFree(x->bounce[i]);
+      x->bounce[i] = nullptr;
+    }
+    x->bounce_cap = 0;
+    for (int i = 0; i < xrs_codec::kPipe; ++i)
+      if (hipHostMalloc(reinterpret_cast<void**>(&x->bounce[i]), bounce, hipHostMallocDefault) != hipSuccess)
+        return XRS_ERR_HIP;
+    x->bounce_cap = bounce;
+  }
   return XRS_OK;
 }
 
-// One strided row copy for a chunk: `rows` stripes, `width` bytes each.
-int copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
-           hipMemcpyKind kind, hipStream_t s) {
-  if (width == 0 || rows == 0) return XRS_OK;
-  return hip_err(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s));
+// ----------------------------------------------------- DMA-clean row copies
+// The runtime's rectangular DMA copy (hipMemcpy2DAsync) needs both row bases
+// 4-byte aligned and both pitches multiples of 4 (any width is fine).  A
+// misaligned base is refused ("DMA buffer failed with code 4097") and the
+// copy falls back to 5.6 GB/s H2D, 12-14 GB/s D2H; a pitch that is not a
+// multiple of 4 runs row by row at 0.56-0.61 GB/s; aligned copies run at
+// 47-49 GB/s (tools/dma_rect_probe.cpp, profiles/r06_dma_rect_probe.log).
+// Odd vect sizes put rows on every residue, so the copies below keep every
+// rectangle aligned for any host layout, given a device image whose rows
+// have the host rows' address residues mod 4 (dev = host, dpitch = hpitch,
+// mod 4; or a mirror of the host bytes, as the queue's staging is):
+//  * a row set is split into k = 1, 2 or 4 pitch groups (every k-th row), so
+//    every group's pitches are multiples of 4;
+//  * host to device, each row starts at its enclosing aligned word (at most 3
+//    bytes more, read from the same word; the device image has slack there);
+//  * device to host, the aligned body of each row is copied straight back,
+//    and its 1-3 head bytes go through a pinned bounce buffer that the CPU
+//    writes back once the stream has finished (HeadFix) -- or, into a mirror,
+//    widened like host to device.
+inline size_t res4(const void* p) { return reinterpret_cast<uintptr_t>(p) & 3u; }
+inline size_t pitch_groups(size_t a, size_t b) {
+  const size_t r = (a | b) & 3u;
+  return r == 0 ? 1 : (r & 1u) ? 4 : 2;
 }
 
-struct HostBatch {
-  uint8_t* base;
-  size_t size, shard_stride, stripe_stride, n_stripes;
-  uint8_t* row(size_t stripe, int shard, size_t off) const {
-    return base + stripe * stripe_stride + static_cast<size_t>(shard) * shard_stride + off;
+// Head bytes of device-to-host rows whose host start is not 4-byte aligned:
+// rows t < rows of the group at host + t * pitch get n bytes from
+// words + 4 * t + m once the copies into `words` have finished.
+struct HeadFix {
+  uint8_t* host;
+  size_t pitch, rows, m, n;
+  const uint8_t* words;
+};
+struct HeadBounce {
+  uint8_t* buf = nullptr;  // pinned
+  size_t cap = 0, used = 0;
+  std::vector<HeadFix> fixes;
+  uint8_t* take(size_t n) {
+    if (!buf || used + n > cap) return nullptr;
+    uint8_t* p = buf + used;
+    used += n;
+    return p;
+  }
+  void apply() {
+    for (const HeadFix& f : fixes)
+      for (size_t t = 0; t < f.rows; ++t) std::memcpy(f.host + t * f.pitch, f.words + 4 * t + f.m, f.n);
+    fixes.clear();
+    used = 0;
   }
 };
+
+// `rows` rows of `len` bytes between host (row r at host + r * hp) and device
+// (dev + r * dp).  H2D always widens; D2H widens when `mirror`, else it takes
+// the head bytes through `hb`.
+int copy_rows(hipMemcpyKind kind, uint8_t* dev, size_t dp, uint8_t* host, size_t hp, size_t len,
+              size_t rows, hipStream_t s, bool mirror, HeadBounce* hb) {
+  if (!len || !rows) return XRS_OK;
+  const size_t k = pitch_groups(hp, dp);
+  for (size_t g = 0; g < k && g < rows; ++g) {
+    uint8_t* h = host + g * hp;
+    uint8_t* d = dev + g * dp;
+    const size_t n = (rows - g + k - 1) / k, m = res4(h);
+    if (res4(d) != m) return XRS_ERR_INVALID_ARG;  // (the image guarantees it)
+    hipError_t r = hipSuccess;
+    if (kind == hipMemcpyHostToDevice || mirror) {
+      const size_t w = m + len;  // (the width needs no alignment)
+      r = kind == hipMemcpyHostToDevice
+              ? hipMemcpy2DAsync(d - m, k * dp, h - m, k * hp, w, n, kind, s)
+              : hipMemcpy2DAsync(h - m, k * hp, d - m, k * dp, w, n, kind, s);
+    } else if (m == 0) {
+      r = hipMemcpy2DAsync(h, k * hp, d, k * dp, len, n, kind, s);
+    } else {
+      const size_t head = std::min(4 - m, len);
+      if (len > head) r = hipMemcpy2DAsync(h + head, k * hp, d + head, k * dp, len - head, n, kind, s);
+      uint8_t* words = hb ? hb->take(4 * n) : nullptr;
+      if (!words) return XRS_ERR_INVALID_ARG;
+      if (r == hipSuccess) r = hipMemcpy2DAsync(words, 4, d - m, k * dp, 4, n, kind, s);
+      hb->fixes.push_back({h, k * hp, n, m, head, words});
+    }
+    if (r != hipSuccess) return XRS_ERR_HIP;
+  }
+  return XRS_OK;
+}
+
+// The device image of a set of host rows that share one stripe pitch: row j
+// of stripe s at host0[j] + s * hp on the host, at chunk_slot + region +
+// off[j] + s * dp on the device.
+//  * compact (every copy of the op is already DMA-clean in it): rows back to
+//    back from the odd-size base offset, as a recommended device batch
+//    (half_align_offset) -- the layout the pipeline always had;
+//  * otherwise residue-matched: off[j] = host0[j] and dp = hp (mod 4), 32 B
+//    of slack around every row, the b-half on the 16-byte boundary where the
+//    residue allows it.
+struct Image {
+  std::vector<uint8_t*> host0;
+  size_t hp = 0, len = 0;  // host pitch, row (vect) length
+  bool compact = true;
+  std::vector<size_t> off;
+  size_t dp = 0, region = 0;
+};
+// A copy of part of row `row` of image `im`: bytes [at, at + len).
+struct Piece {
+  int im, row;
+  size_t at, len;
+};
+
+void plan_image(Image* im, const std::vector<Piece>& pieces, int idx) {
+  const size_t S = im->len, H = S / 2, m = im->host0.size(), bo = half_align_offset(S);
+  bool clean = (im->hp & 3u) == 0 && ((m * S) & 3u) == 0;
+  for (const Piece& p : pieces)
+    if (p.im == idx)
+      clean = clean && res4(im->host0[p.row] + p.at) == 0 && ((bo + p.row * S + p.at) & 3u) == 0;
+  im->compact = clean;
+  im->off.assign(m, 0);
+  if (clean) {
+    for (size_t j = 0; j < m; ++j) im->off[j] = bo + j * S;
+    im->dp = m * S;
+    return;
+  }
+  const size_t S16 = ((S + 15) & ~size_t(15)) + 32, t = (16 - H % 16) % 16;
+  for (size_t j = 0; j < m; ++j) {
+    const size_t o = (t + ((res4(im->host0[j]) - t) & 3u)) & 15u;  // = host0[j] (mod 4)
+    im->off[j] = 16 + j * S16 + o;
+  }
+  im->dp = 16 + m * S16 + (im->hp & 3u);  // = hp (mod 4)
+}
+
+// The op's layout over image `im` in a chunk slot (tab: per-row bases of a
+// residue-matched image, which Layout reads at launch).
+Layout image_layout(const Image& im, uint8_t* slot, std::vector<uint64_t>* tab) {
+  if (im.compact) return {slot + im.region + im.off[0], im.len, im.dp};
+  tab->resize(im.off.size());
+  for (size_t j = 0; j < im.off.size(); ++j)
+    (*tab)[j] = reinterpret_cast<uint64_t>(slot + im.region + im.off[j]);
+  return {nullptr, 0, im.dp, tab->data()};
+}
 
 // Chunked H2D -> kernel -> D2H over kPipe streams.  `in` / `out` list the
-// (shard, half) pieces moved per stripe (half: 0 = a, 1 = b, 2 = whole vect);
-// `launch(slot_base, n, stream)` runs the op on the compact device layout.
+// pieces moved per stripe; launch(slot, n, stream) runs the op on the chunk's
+// device images (image_layout).  Images and pieces as above.
 template <class Launch>
-int run_pipeline(const xrs_codec* x, const HostBatch& hb,
-                 const std::vector<std::pair<int, int>>& in,
-                 const std::vector<std::pair<int, int>>& out, Launch launch) {
-  const int nshards = x->d + x->p;
-  const size_t S = hb.size, H = S / 2;
-  const size_t dev_stripe = static_cast<size_t>(nshards) * S;
-  const size_t chunk = std::max<size_t>(1, std::min(hb.n_stripes, kChunkBytes / dev_stripe));
-  std::lock_guard<std::mutex> lk(x->pipe_mu);
-  DeviceGuard g(x->device);
-  // device slots start at the odd-size base offset (half_align_offset)
-  const size_t bo = half_align_offset(S);
-  int e = ensure_pipe(x, chunk * dev_stripe + bo);
-  if (e) return e;
-  auto piece = [&](int half, size_t* off, size_t* len) {
-    *off = half == 1 ? H : 0;
-    *len = half == 2 ? S : H;
-  };
-  size_t i = 0;
-  for (size_t c0 = 0; c0 < hb.n_stripes && !e; c0 += chunk, ++i) {
-    const int si = static_cast<int>(i % xrs_codec::kPipe);
-    hipStream_t st = x->pstream[si];
-    uint8_t* slot = x->slot[si] + bo;
-    const size_t nc = std::min(chunk, hb.n_stripes - c0);
-    for (auto& p : in) {
-      size_t off, len;
-      piece(p.second, &off, &len);
-      if ((e = copy2d(slot + static_cast<size_t>(p.first) * S + off, dev_stripe,
-                      hb.row(c0, p.first, off), hb.stripe_stride, len, nc,
-                      hipMemcpyHostToDevice, st)))
-        break;
-    }
-    if (!e) e = launch(slot, nc, st);
-    for (auto& p : out) {
-      if (e) break;
-      size_t off, len;
-      piece(p.second, &off, &len);
-      e = copy2d(hb.row(c0, p.first, off), hb.stripe_stride,
-                 slot + static_cast<size_t>(p.first) * S + off, dev_stripe, len, nc,
-                 hipMemcpyDeviceToHost, st);
-    }
+int run_pipeline(const xrs_codec* x, std::vector<Image>& ims, size_t n_stripes,
+                 const std::vector<Piece>& in, const std::vector<Piece>& out, Launch launch) {
+  std::vector<Piece> all(in);
+  all.insert(all.end(), out.begin(), out.end());
+  size_t dev_stripe = 0;
+  for (size_t i = 0; i < ims.size(); ++i) {
+    plan_image(&ims[i], all, static_cast<int>(i));
+    dev_stripe += ims[i].dp;
   }
-  int es = XRS_OK;
-  for (int k = 0; k < xrs_codec::kPipe; ++k)
-    if (hipStreamSynchronize(x->pstream[k]) != hipSuccess) es = XRS_ERR_HIP;
-  return e ? e : es;
-}
-
-// A host row stream of a batch: stripe s of it is `len` bytes at
-// host + s * stride, staged at dev_off of the stripe's compact device slot.
-struct HostRows {
-  uint8_t* host;
-  size_t stride;
-  size_t dev_off, len;
-};
-
-// run_pipeline for operations whose rows live in separate host buffers
-// (Update: old, new and parity; Replace: data and parity): chunked H2D of
-// `in`, launch(slot, n, stream) on stripes of dev_stripe bytes, D2H of `out`.
-template <class Launch>
-int run_pipeline_rows(const xrs_codec* x, size_t size, size_t n_stripes, size_t dev_stripe,
-                      const std::vector<HostRows>& in, const std::vector<HostRows>& out,
-                      Launch launch) {
   const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
+  size_t bytes = 0;
+  for (Image& im : ims) {  // each image's chunk region, 256-byte aligned
+    im.region = bytes;
+    bytes += (chunk * im.dp + 255) & ~size_t(255);
+  }
   std::lock_guard<std::mutex> lk(x->pipe_mu);
   DeviceGuard g(x->device);
-  const size_t bo = half_align_offset(size);  // as run_pipeline
-  int e = ensure_pipe(x, chunk * dev_stripe + bo);
+  int e = ensure_pipe(x, bytes, std::max<size_t>(4096, out.size() * chunk * 4));
   if (e) return e;
+  HeadBounce hb[xrs_codec::kPipe];
+  for (int k = 0; k < xrs_codec::kPipe; ++k) {
+    hb[k].buf = x->bounce[k];
+    hb[k].cap = x->bounce_cap;
+  }
   size_t i = 0;
   for (size_t c0 = 0; c0 < n_stripes && !e; c0 += chunk, ++i) {
     const int si = static_cast<int>(i % xrs_codec::kPipe);
     hipStream_t st = x->pstream[si];
-    uint8_t* slot = x->slot[si] + bo;
+    if (!hb[si].fixes.empty()) {  // this slot's previous chunk: its head bytes
+      if (hipStreamSynchronize(st) != hipSuccess) {
+        e = XRS_ERR_HIP;
+        break;
+      }
+      hb[si].apply();
+    }
+    uint8_t* slot = x->slot[si];
     const size_t nc = std::min(chunk, n_stripes - c0);
-    for (const HostRows& r : in)
+    auto dev_at = [&](const Piece& p) {
+      const Image& im = ims[p.im];
+      return slot + im.region + im.off[p.row] + p.at;
+    };
+    auto host_at = [&](const Piece& p) {
+      const Image& im = ims[p.im];
+      return im.host0[p.row] + c0 * im.hp + p.at;
+    };
+    for (const Piece& p : in)
       if (!e)
-        e = copy2d(slot + r.dev_off, dev_stripe, r.host + c0 * r.stride, r.stride, r.len, nc,
-                   hipMemcpyHostToDevice, st);
+        e = copy_rows(hipMemcpyHostToDevice, dev_at(p), ims[p.im].dp, host_at(p), ims[p.im].hp,
+                      p.len, nc, st, false, nullptr);
     if (!e) e = launch(slot, nc, st);
-    for (const HostRows& r : out)
+    for (const Piece& p : out)
       if (!e)
-        e = copy2d(r.host + c0 * r.stride, r.stride, slot + r.dev_off, dev_stripe, r.len, nc,
-                   hipMemcpyDeviceToHost, st);
+        e = copy_rows(hipMemcpyDeviceToHost, dev_at(p), ims[p.im].dp, host_at(p), ims[p.im].hp,
+                      p.len, nc, st, false, &hb[si]);
   }
   int es = XRS_OK;
   for (int k = 0; k < xrs_codec::kPipe; ++k)
     if (hipStreamSynchronize(x->pstream[k]) != hipSuccess) es = XRS_ERR_HIP;
+  if (!e && !es)
+    for (HeadBounce& b : hb) b.apply();
   return e ? e : es;
+}
+
+// One image of a host batch's d+p shards (shard j of stripe s at base +
+// s * stripe_stride + j * shard_stride), and its pieces: (shard, half) with
+// half 0 = a, 1 = b, 2 = the whole vect.
+Image batch_image(const xrs_codec* x, uint8_t* base, size_t size, size_t shard_stride,
+                  size_t stripe_stride) {
+  Image im;
+  for (int j = 0; j < x->d + x->p; ++j) im.host0.push_back(base + static_cast<size_t>(j) * shard_stride);
+  im.hp = stripe_stride;
+  im.len = size;
+  return im;
+}
+std::vector<Piece> halves(const std::vector<std::pair<int, int>>& hs, size_t size) {
+  std::vector<Piece> v;
+  for (const auto& h : hs)
+    v.push_back({0, h.first, h.second == 1 ? size / 2 : 0, h.second == 2 ? size : size / 2});
+  return v;
 }
 
 bool vects_ok(uint8_t* const* v, int n) {
@@ -1013,6 +1139,13 @@ int replace_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, co
   const Layout P{nullptr, 0, 0, nullptr, tab, tab_stride};
   const Layout D{nullptr, 0, 0, nullptr, tab + 2 * x->p, tab_stride};
   return replace_impl(x, D, rows, n_rows, size, P, n, static_cast<hipStream_t>(stream));
+}
+// The queue's staging copies (its pinned staging and device batch are
+// mirrors: same offsets, same pitch): DMA-clean for any vect size.
+int copy_rows_mirror(bool to_device, uint8_t* dev, uint8_t* host, size_t pitch, size_t len,
+                     size_t rows, void* stream) {
+  return copy_rows(to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, dev, pitch, host,
+                   pitch, len, rows, static_cast<hipStream_t>(stream), true, nullptr);
 }
 int codec_device(const xrs_codec* x) { return x->device; }
 int codec_d(const xrs_codec* x) { return x->d; }
@@ -1113,6 +1246,7 @@ void xrs_free(xrs_codec* x) {
     for (int i = 0; i < xrs_codec::kPipe; ++i) {
       if (x->pstream[i]) (void)hipStreamDestroy(x->pstream[i]);
       if (x->slot[i]) (void)hipFree(x->slot[i]);
+      if (x->bounce[i]) (void)hipHostFree(x->bounce[i]);
     }
   }
   delete x;
@@ -1528,10 +1662,11 @@ int xrs_encode_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t 
     return run_in_place(x, [&](hipStream_t s) {
       return encode_impl(x, {zb, shard_stride, stripe_stride}, size, n_stripes, s);
     });
-  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
-  const size_t dev_stripe = static_cast<size_t>(d + p) * size;
-  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
-    return encode_impl(x, {slot, size, dev_stripe}, size, n, s);
+  std::vector<Image> ims = {batch_image(x, host_base, size, shard_stride, stripe_stride)};
+  std::vector<uint64_t> tab;
+  return run_pipeline(x, ims, n_stripes, halves(in, size), halves(out, size),
+                      [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return encode_impl(x, image_layout(ims[0], slot, &tab), size, n, s);
   });
 }
 
@@ -1546,7 +1681,7 @@ int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, si
   if (n_stripes == 0 || size == 0) return XRS_OK;
   if (!host_base) return XRS_ERR_INVALID_ARG;
   if (x->device < 0) return XRS_ERR_NO_DEVICE;
-  const int d = x->d, p = x->p;
+  const int d = x->d;
   // Only the GetNeedVects set crosses PCIe (xrs.go:146-171).
   std::vector<std::pair<int, int>> in, out = {{k, 2}};
   for (int m = 0; m < d; ++m) in.push_back({m == k ? d : m, 1});
@@ -1556,10 +1691,11 @@ int xrs_reconst_one_host(const xrs_codec* x, uint8_t* host_base, size_t size, si
     return run_in_place(x, [&](hipStream_t s) {
       return reconst_one_impl(x, {zb, shard_stride, stripe_stride}, size, n_stripes, k, s);
     });
-  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
-  const size_t dev_stripe = static_cast<size_t>(d + p) * size;
-  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
-    return reconst_one_impl(x, {slot, size, dev_stripe}, size, n, k, s);
+  std::vector<Image> ims = {batch_image(x, host_base, size, shard_stride, stripe_stride)};
+  std::vector<uint64_t> tab;
+  return run_pipeline(x, ims, n_stripes, halves(in, size), halves(out, size),
+                      [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return reconst_one_impl(x, image_layout(ims[0], slot, &tab), size, n, k, s);
   });
 }
 
@@ -1613,10 +1749,12 @@ int xrs_reconst_host(const xrs_codec* x, uint8_t* host_base, size_t size, size_t
       return reconst_impl(x, {zb, shard_stride, stripe_stride}, size, n_stripes, dp_has, n_has,
                           need, n_need, s, &w);
     });
-  const HostBatch hb{host_base, size, shard_stride, stripe_stride, n_stripes};
-  const size_t dev_stripe = static_cast<size_t>(m) * size;
-  return run_pipeline(x, hb, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
-    return reconst_impl(x, {slot, size, dev_stripe}, size, n, dp_has, n_has, need, n_need, s, &w);
+  std::vector<Image> ims = {batch_image(x, host_base, size, shard_stride, stripe_stride)};
+  std::vector<uint64_t> tab;
+  return run_pipeline(x, ims, n_stripes, halves(in, size), halves(out, size),
+                      [&](uint8_t* slot, size_t n, hipStream_t s) {
+    return reconst_impl(x, image_layout(ims[0], slot, &tab), size, n, dp_has, n_has, need, n_need,
+                        s, &w);
   });
 }
 
@@ -1646,22 +1784,26 @@ int xrs_update_host(const xrs_codec* x, const uint8_t* old_base, size_t old_stri
                          {reinterpret_cast<uint64_t>(zn), new_stripe_stride}, size, row,
                          {zp, parity_shard_stride, parity_stripe_stride}, n_stripes, s);
     });
-  // device stripe: p parity rows, then old, then new
-  const size_t dev_stripe = static_cast<size_t>(p + 2) * size;
-  std::vector<HostRows> in, out;
+  // device images: the p parity rows, old, new (each its own host pitch)
+  std::vector<Image> ims(3);
+  for (int r = 0; r < p; ++r) ims[0].host0.push_back(parity_base + r * parity_shard_stride);
+  ims[0].hp = parity_stripe_stride;
+  ims[1].host0 = {const_cast<uint8_t*>(old_base)};
+  ims[1].hp = old_stripe_stride;
+  ims[2].host0 = {const_cast<uint8_t*>(new_base)};
+  ims[2].hp = new_stripe_stride;
+  for (Image& im : ims) im.len = size;
+  std::vector<Piece> in, out;
   for (int r = 0; r < p; ++r) {
-    const HostRows pr{parity_base + r * parity_shard_stride, parity_stripe_stride,
-                      static_cast<size_t>(r) * size, size};
-    in.push_back(pr);
-    out.push_back(pr);
+    in.push_back({0, r, 0, size});
+    out.push_back({0, r, 0, size});
   }
-  in.push_back({const_cast<uint8_t*>(old_base), old_stripe_stride, static_cast<size_t>(p) * size, size});
-  in.push_back({const_cast<uint8_t*>(new_base), new_stripe_stride, static_cast<size_t>(p + 1) * size, size});
-  return run_pipeline_rows(x, size, n_stripes, dev_stripe, in, out,
-                           [&](uint8_t* slot, size_t n, hipStream_t s) {
-    return update_impl(x, {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p) * size), dev_stripe},
-                       {reinterpret_cast<uint64_t>(slot + static_cast<size_t>(p + 1) * size), dev_stripe},
-                       size, row, {slot, size, dev_stripe}, n, s);
+  in.push_back({1, 0, 0, size});
+  in.push_back({2, 0, 0, size});
+  std::vector<uint64_t> tp, to, tn;
+  return run_pipeline(x, ims, n_stripes, in, out, [&](uint8_t* slot, size_t n, hipStream_t s) {
+    const Layout o = image_layout(ims[1], slot, &to), nw = image_layout(ims[2], slot, &tn);
+    return update_impl(x, o.row(0, 0), nw.row(0, 0), size, row, image_layout(ims[0], slot, &tp), n, s);
   });
 }
 
@@ -1688,22 +1830,24 @@ int xrs_replace_host(const xrs_codec* x, const uint8_t* data_base, size_t data_s
       return replace_impl(x, {zd, data_shard_stride, data_stripe_stride}, rows, n, size,
                           {zp, parity_shard_stride, parity_stripe_stride}, n_stripes, s);
     });
-  // device stripe: p parity rows, then the n data rows
-  const size_t dev_stripe = static_cast<size_t>(p + n) * size;
-  std::vector<HostRows> in, out;
-  for (int r = 0; r < p; ++r) {
-    const HostRows pr{parity_base + r * parity_shard_stride, parity_stripe_stride,
-                      static_cast<size_t>(r) * size, size};
-    in.push_back(pr);
-    out.push_back(pr);
-  }
+  // device images: the p parity rows, the n data rows
+  std::vector<Image> ims(2);
+  for (int r = 0; r < p; ++r) ims[0].host0.push_back(parity_base + r * parity_shard_stride);
+  ims[0].hp = parity_stripe_stride;
   for (int i = 0; i < n; ++i)
-    in.push_back({const_cast<uint8_t*>(data_base) + i * data_shard_stride, data_stripe_stride,
-                  static_cast<size_t>(p + i) * size, size});
-  return run_pipeline_rows(x, size, n_stripes, dev_stripe, in, out,
-                           [&](uint8_t* slot, size_t ns, hipStream_t s) {
-    return replace_impl(x, {slot + static_cast<size_t>(p) * size, size, dev_stripe}, rows, n, size,
-                        {slot, size, dev_stripe}, ns, s);
+    ims[1].host0.push_back(const_cast<uint8_t*>(data_base) + i * data_shard_stride);
+  ims[1].hp = data_stripe_stride;
+  for (Image& im : ims) im.len = size;
+  std::vector<Piece> in, out;
+  for (int r = 0; r < p; ++r) {
+    in.push_back({0, r, 0, size});
+    out.push_back({0, r, 0, size});
+  }
+  for (int i = 0; i < n; ++i) in.push_back({1, i, 0, size});
+  std::vector<uint64_t> tp, td;
+  return run_pipeline(x, ims, n_stripes, in, out, [&](uint8_t* slot, size_t ns, hipStream_t s) {
+    return replace_impl(x, image_layout(ims[1], slot, &td), rows, n, size,
+                        image_layout(ims[0], slot, &tp), ns, s);
   });
 }
 

@@ -1,9 +1,12 @@
 // hostreg.cpp -- the registered host ranges (hostreg.h).
 #include "hostreg.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace xrs_detail {
@@ -16,41 +19,52 @@ struct Range {
 using Table = std::vector<Range>;
 
 // Reader counts, striped over cache lines so concurrent callers do not share
-// one.  Every operation is seq_cst: a reader increments its lane before it
-// loads the table pointer, and a writer swaps the pointer before it reads the
-// lanes, so a reader the writer sees at zero loads the new table.
+// one, in two generations.  A reader increments its lane's count of the
+// current generation, then loads the table pointer, and holds both for one
+// call's lookups (microseconds).  A writer swaps the pointer, then makes two
+// grace periods: flip the generation and wait until the old generation's
+// counts are all zero, twice.  A reader that loaded the replaced table had
+// incremented a count (of either generation) before the swap, and each
+// generation is waited for after the swap, so the replaced table is freed at
+// once, with no reader on it; readers arriving meanwhile count in the other
+// generation, so under steady traffic each wait ends (the round-5
+// table waited for all 16 lanes to read zero at once, which steady traffic
+// may never give, and retired tables could pile up).  Every operation is
+// seq_cst.
 constexpr unsigned kLanes = 16;
 struct alignas(64) Lane {
-  std::atomic<uint32_t> n{0};
+  std::atomic<uint32_t> n[2] = {{0}, {0}};
 };
 Lane g_lanes[kLanes];
 std::atomic<unsigned> g_next_lane{0};
+std::atomic<unsigned> g_gen{0};
 
 std::atomic<const Table*> g_table{nullptr};
 std::mutex g_mu;
-std::vector<const Table*> g_retired;  // (g_mu) replaced, maybe still read
 
 unsigned my_lane() {
   thread_local const unsigned lane = g_next_lane.fetch_add(1, std::memory_order_relaxed) % kLanes;
   return lane;
 }
 
-bool quiescent() {
+void drain(unsigned gen) {  // (a view lasts microseconds: spin first)
   for (const Lane& l : g_lanes)
-    if (l.n.load()) return false;
-  return true;
+    for (unsigned i = 0; l.n[gen].load(); ++i) {
+      if (i < 4096) _mm_pause();
+      else std::this_thread::yield();
+    }
 }
 
 void publish(Table* t) {  // (g_mu held)
   std::sort(t->begin(), t->end(), [](const Range& a, const Range& b) { return a.lo < b.lo; });
   const Table* old = g_table.exchange(t);
-  if (old) g_retired.push_back(old);
-  // a reader still holding a retired table keeps its lane above zero; any
-  // reader arriving later loads t
-  if (quiescent()) {
-    for (const Table* r : g_retired) delete r;
-    g_retired.clear();
+  if (!old) return;
+  for (int phase = 0; phase < 2; ++phase) {
+    const unsigned g = g_gen.load();
+    g_gen.store(g ^ 1u);
+    drain(g);
   }
+  delete old;
 }
 
 }  // namespace
@@ -81,11 +95,12 @@ void host_ranges_remove(const void* p) {
 }
 
 HostRangesView::HostRangesView() : lane_(my_lane()) {
-  g_lanes[lane_].n.fetch_add(1);
+  gen_ = g_gen.load();
+  g_lanes[lane_].n[gen_].fetch_add(1);
   table_ = g_table.load();
 }
 
-HostRangesView::~HostRangesView() { g_lanes[lane_].n.fetch_sub(1); }
+HostRangesView::~HostRangesView() { g_lanes[lane_].n[gen_].fetch_sub(1); }
 
 uint64_t HostRangesView::device(const void* p, size_t bytes) const {
   const Table* t = static_cast<const Table*>(table_);
@@ -99,9 +114,6 @@ uint64_t HostRangesView::device(const void* p, size_t bytes) const {
   return it->dev + (a - it->lo);
 }
 
-size_t host_ranges_retired() {
-  std::lock_guard<std::mutex> g(g_mu);
-  return g_retired.size();
-}
+size_t host_ranges_retired() { return 0; }  // (replaced tables are freed in publish)
 
 }  // namespace xrs_detail

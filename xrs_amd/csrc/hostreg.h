@@ -7,8 +7,10 @@
 // queue batch through its row table), addressed by the device pointer
 // recorded here.  A lookup takes no lock and makes no HIP call: an immutable
 // sorted table behind an atomic pointer, which register / unregister replace.
-// A replaced table is freed once no lookup can still hold it (HostRangesView
-// keeps a reader count on one of a few cache lines).
+// A replaced table is freed by the register / unregister that replaced it,
+// after a grace period: HostRangesView keeps a reader count (one of a few
+// cache lines, two generations) for the few microseconds of one call's
+// lookups, and the writer waits for the counts that may cover the old table.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -33,10 +35,10 @@ class HostRangesView {
 
  private:
   const void* table_;
-  unsigned lane_;
+  unsigned lane_, gen_;
 };
 
-// Retired tables not yet freed (tests).
+// Replaced tables not yet freed (tests; always 0 since round 6).
 size_t host_ranges_retired();
 
 }  // namespace xrs_detail

@@ -76,6 +76,8 @@ int update_rows_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride
                       const int32_t* rows, size_t n, void* stream);
 int replace_table(const xrs_codec* x, const uint64_t* tab, size_t tab_stride, const int* rows,
                   int n_rows, size_t size, size_t n, void* stream);
+int copy_rows_mirror(bool to_device, uint8_t* dev, uint8_t* host, size_t pitch, size_t len,
+                     size_t rows, void* stream);
 int codec_device(const xrs_codec* x);
 int codec_d(const xrs_codec* x);
 int codec_p(const xrs_codec* x);
@@ -152,6 +154,12 @@ struct Batch {
   // when the batch's results are in staging; err and n are written first)
   std::atomic<uint32_t> filled{0}, released{0}, done{0};
   std::atomic<uint32_t> n_reg{0};  // slots whose vects are all in registered memory
+  // Asynchronous registered slots (nothing to copy back): released by the
+  // completion thread itself when the batch succeeds, so their batch is
+  // recycled without waiting for the tickets' owners (auto_st[slot]: the
+  // ticket's status word, else nullptr).
+  std::vector<std::atomic<int>*> auto_st;
+  std::atomic<uint32_t> n_auto{0};
   size_t n = 0;  // slots of the closed batch
   int err = 0;
 };
@@ -220,12 +228,14 @@ struct xrs_queue {
     size_t slot = 0;
     uint32_t seq = 0;
     bool reg = false;  // the call's vects are registered: no copies
+    std::atomic<int>* status = nullptr;  // auto-released slot: 0 once done
     std::vector<Piece> out;
   };
   // Reserve a slot and stage the call (no wait).  nonblock: XRS_ERR_BUSY
   // instead of waiting for a free staging batch.
   int stage(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
-            const std::vector<int>* has, const std::vector<int>* need, bool nonblock, Staged* sc);
+            const std::vector<int>* has, const std::vector<int>* need, bool nonblock, Staged* sc,
+            std::atomic<int>* status = nullptr);
   // Wait for a staged call's batch, copy its outputs back, release the slot.
   int wait(Staged& sc);
   int submit(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row = -1,
@@ -246,6 +256,7 @@ struct xrs_queue_ticket {
   xrs_queue* q = nullptr;
   xrs_queue::Staged st;
   int err = 0;
+  std::atomic<int> status{-1};  // (registered vects: set to 0 by the completion thread)
 };
 
 int xrs_queue::run(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
@@ -255,7 +266,7 @@ int xrs_queue::run(int key, const std::vector<Piece>& in, const std::vector<Piec
   *t = nullptr;
   auto* tk = new xrs_queue_ticket();
   tk->q = this;
-  const int e = stage(key, in, out, row, has, need, true, &tk->st);
+  const int e = stage(key, in, out, row, has, need, true, &tk->st, &tk->status);
   if (e) {
     delete tk;
     return e;
@@ -308,9 +319,9 @@ int xrs_queue::launch(Batch& bt) {
     else
       e = xrs_detail::reconst_one_table(codec, bt.tab_dev, ts, size, n, bt.key - 1, bt.stream);
   } else {
-    if (!zc && hipMemcpy2DAsync(dst + up_off, stripe_bytes, hst + up_off, stripe_bytes, up_len,
-                                n, hipMemcpyHostToDevice, bt.stream) != hipSuccess)
-      e = XRS_ERR_HIP;
+    if (!zc)  // (odd sizes: rows start at an aligned word, codec.cpp copy_rows)
+      e = xrs_detail::copy_rows_mirror(true, dst + up_off, hst + up_off, stripe_bytes, up_len, n,
+                                       bt.stream);
     if (!e) {
       if (enc)
         e = xrs_detail::encode_dev(codec, base, size, size, stripe_bytes, n, bt.stream);
@@ -330,10 +341,9 @@ int xrs_queue::launch(Batch& bt) {
         e = xrs_detail::reconst_one_dev(codec, base, size, size, stripe_bytes, n, bt.key - 1,
                                         bt.stream);
     }
-    if (!e && !zc &&
-        hipMemcpy2DAsync(hst + dn_off, stripe_bytes, dst + dn_off, stripe_bytes, dn_len, n,
-                         hipMemcpyDeviceToHost, bt.stream) != hipSuccess)
-      e = XRS_ERR_HIP;
+    if (!e && !zc)
+      e = xrs_detail::copy_rows_mirror(false, dst + dn_off, hst + dn_off, stripe_bytes, dn_len, n,
+                                       bt.stream);
   }
   if (!e && hipStreamWriteValue32(bt.stream, bt.flag_dev, ++bt.launches, 0) != hipSuccess)
     e = XRS_ERR_HIP;
@@ -344,19 +354,31 @@ int xrs_queue::launch(Batch& bt) {
 // Batch i's results are in staging (or it failed): release its callers.
 void xrs_queue::finish(int i, int err) {
   Batch& bt = b[i];
+  const size_t n = bt.n;
+  const uint32_t n_auto = err ? 0 : bt.n_auto.load(std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> lk(mu);
     bt.err = err;
     bt.state = DONE;
     --in_flight;
     ++st_batches;
-    st_stripes += bt.n;
-    ++st_hist[std::min<size_t>(bt.n, kHist - 1)];
+    st_stripes += n;
+    ++st_hist[std::min<size_t>(n, kHist - 1)];
     st_run_ns += ns_since(bt.launched);
     cv_work.notify_one();  // a launcher may wait for in_flight < max_inflight
   }
+  if (n_auto)  // asynchronous registered calls: done, nothing to copy back
+    for (size_t j = 0; j < n; ++j)
+      if (bt.auto_st[j]) bt.auto_st[j]->store(0, std::memory_order_relaxed);
   bt.done.fetch_add(1, std::memory_order_release);
   futex_wake_all(&bt.done);
+  // their slots are released here, after the completion count moved (a batch
+  // recycled before it would wake the next calls' waiters), once per slot
+  if (n_auto && bt.released.fetch_add(n_auto, std::memory_order_acq_rel) + n_auto == n) {
+    std::lock_guard<std::mutex> lk(mu);
+    bt.state = FREE;
+    cv_free.notify_all();
+  }
 }
 
 void xrs_queue::work() {
@@ -477,7 +499,7 @@ void xrs_queue::complete() {
 
 int xrs_queue::stage(int key, const std::vector<Piece>& in, const std::vector<Piece>& out, int row,
                      const std::vector<int>* has, const std::vector<int>* need, bool nonblock,
-                     Staged* sc) {
+                     Staged* sc, std::atomic<int>* status) {
   auto same_pattern = [&](const Batch& bt) {
     return !has || (bt.pat_has == *has && bt.pat_need == *need);
   };
@@ -531,6 +553,7 @@ int xrs_queue::stage(int key, const std::vector<Piece>& in, const std::vector<Pi
       nb.released.store(0, std::memory_order_relaxed);
       nb.err = 0;
       nb.n_reg.store(0, std::memory_order_relaxed);
+      nb.n_auto.store(0, std::memory_order_relaxed);
       nb.opened = Clock::now();
       if (has) {
         nb.pat_has = *has;
@@ -558,6 +581,9 @@ int xrs_queue::stage(int key, const std::vector<Piece>& in, const std::vector<Pi
       }
     if (reg) bt.n_reg.fetch_add(1, std::memory_order_relaxed);
   }
+  // (every reservation sets its entry: the vector keeps entries of earlier batches)
+  bt.auto_st[slot] = reg && status ? status : nullptr;
+  if (reg && status) bt.n_auto.fetch_add(1, std::memory_order_relaxed);
   if (!reg)
     for (const Piece& pc : in)
       std::memcpy(st + static_cast<size_t>(pc.row) * size + pc.off, pc.host + pc.off, pc.len);
@@ -571,6 +597,7 @@ int xrs_queue::stage(int key, const std::vector<Piece>& in, const std::vector<Pi
   sc->slot = slot;
   sc->seq = seq;
   sc->reg = reg;
+  sc->status = reg && status ? status : nullptr;
   sc->out = out;
   return XRS_OK;
 }
@@ -582,6 +609,12 @@ int xrs_queue::wait(Staged& sc) {
   const std::vector<Piece>& out = sc.out;
   uint8_t* st = bt.host + bo + sc.slot * stripe_bytes;
   while (bt.done.load(std::memory_order_acquire) == seq) futex_wait(&bt.done, seq);
+  if (sc.status && sc.status->load(std::memory_order_acquire) == 0) {
+    // released by the completion thread (the batch may be running new calls
+    // already): nothing of it is touched here
+    leave();
+    return XRS_OK;
+  }
   // The batch cannot be recycled before this caller's own release below, so
   // its slot count and status are read here, once: after the release another
   // caller may free the batch and a new submit() reopen it (n = 0).
@@ -666,6 +699,7 @@ int xrs_queue_new(const xrs_codec* codec, size_t size, size_t max_batch_stripes,
       break;
     }
     bt.rows_dev = static_cast<int32_t*>(dp);
+    bt.auto_st.assign(q->max_batch, nullptr);
     // row tables for registered callers (at most 16 MiB per batch, else the
     // queue copies every call through `host`; XRS_QUEUE_REG=0: always)
     const size_t tb = q->max_batch * 2 * q->nrows * sizeof(uint64_t);

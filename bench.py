@@ -349,6 +349,10 @@ def parse_args(argv=None):
                     help="MiB per host-resident batch for the host_e2e key (0: skip)")
     ap.add_argument("--queue-callers", type=int, nargs="*", default=[32],
                     help="caller threads for the per_stripe_queue key (N = 1 only; none: skip)")
+    ap.add_argument("--async-window", type=int, default=16,
+                    help="stripes each caller keeps in flight in the per_stripe_queue async leg")
+    ap.add_argument("--async-callers", type=int, nargs="*", default=[8],
+                    help="caller threads of the per_stripe_queue async leg")
     ap.add_argument("--xgmi-stripes", type=int, default=64,
                     help="1 MiB stripes for the xgmi_repair key (0: skip)")
     ap.add_argument("--xgmi-child", type=int, default=None, help=argparse.SUPPRESS)
@@ -845,9 +849,9 @@ def per_stripe_queue(args):
     exe = os.path.join(ROOT, "tools", "sync_bench")
     if not os.path.exists(exe):
         return {"skipped": "tools/sync_bench not built (build() makes it)"}
-    def child(mode, size=4096):
-        cmd = [exe, str(size), mode] + (["50"] if mode.startswith("queue") else []) + [
-            str(t) for t in args.queue_callers]
+    def child(mode, size=4096, window=None, callers=None):
+        cmd = [exe, str(size), mode] + (["50"] if mode.startswith("queue") else []) + (
+            [str(window)] if window else []) + [str(t) for t in (callers or args.queue_callers)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
         except subprocess.TimeoutExpired:
@@ -890,6 +894,16 @@ def per_stripe_queue(args):
             "gibps", "stripes_per_batch", "run_us_per_batch", "cpu_cores", "cpu_seconds_per_gib")
             if k in x} for x in lines}
     out["queue_64k"] = big
+    # the asynchronous calls (xrs_queue_submit_encode + xrs_queue_wait): each
+    # caller thread keeps a window of stripes in flight -- one cgo call site
+    # with k stripes outstanding instead of k blocked OS threads
+    asy = {"api": "xrs_queue_submit_encode + xrs_queue_wait", "window": args.async_window}
+    for name, mode in (("plain", "queueasync"), ("registered", "queueasyncreg")):
+        lines, err = child(mode, 4096, args.async_window, args.async_callers)
+        asy[name] = err or {str(x["threads"]): {k: x[k] for k in (
+            "gibps", "stripes_per_batch", "run_us_per_batch", "busy_returns", "cpu_cores",
+            "cpu_seconds_per_gib") if k in x} for x in lines}
+    out["async_4k"] = asy
     return out
 
 

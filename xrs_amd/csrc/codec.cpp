@@ -872,8 +872,9 @@ int ensure_pipe(const xrs_codec* x, size_t bytes, size_t bounce) {
 // rectangle aligned for any host layout, given a device image whose rows
 // have the host rows' address residues mod 4 (dev = host, dpitch = hpitch,
 // mod 4; or a mirror of the host bytes, as the queue's staging is):
-//  * a row set is split into k = 1, 2 or 4 pitch groups (every k-th row), so
-//    every group's pitches are multiples of 4;
+//  * a row set is split into k = 1, 2, 4 (or 8) pitch groups (every k-th
+//    row), so every group's pitches are multiples of 4 and at least as long
+//    as its widened rows;
 //  * host to device, each row starts at its enclosing aligned word (at most 3
 //    bytes more, read from the same word; the device image has slack there);
 //  * device to host, the aligned body of each row is copied straight back,
@@ -918,7 +919,12 @@ struct HeadBounce {
 int copy_rows(hipMemcpyKind kind, uint8_t* dev, size_t dp, uint8_t* host, size_t hp, size_t len,
               size_t rows, hipStream_t s, bool mirror, HeadBounce* hb) {
   if (!len || !rows) return XRS_OK;
-  const size_t k = pitch_groups(hp, dp);
+  // (a widened row may be longer than the pitch -- back-to-back rows, or a
+  // whole staged stripe -- and a rectangle's width may not exceed its pitch:
+  // then every 2nd or 4th row)
+  size_t k = pitch_groups(hp, dp);
+  const size_t slack = (((hp | dp) & 3u) || res4(host)) ? 3 : 0;  // widening, at most
+  while (k < 8 && (k * hp < len + slack || k * dp < len + slack)) k *= 2;
   for (size_t g = 0; g < k && g < rows; ++g) {
     uint8_t* h = host + g * hp;
     uint8_t* d = dev + g * dp;

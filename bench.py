@@ -351,7 +351,7 @@ def parse_args(argv=None):
                     help="caller threads for the per_stripe_queue key (N = 1 only; none: skip)")
     ap.add_argument("--async-window", type=int, default=16,
                     help="stripes each caller keeps in flight in the per_stripe_queue async leg")
-    ap.add_argument("--async-callers", type=int, nargs="*", default=[8],
+    ap.add_argument("--async-callers", type=int, nargs="*", default=[4, 16],
                     help="caller threads of the per_stripe_queue async leg")
     ap.add_argument("--xgmi-stripes", type=int, default=64,
                     help="1 MiB stripes for the xgmi_repair key (0: skip)")

@@ -139,7 +139,12 @@ def _load():
         "xrs_group_replace_host": ([P, P, Z, Z, IP, I, Z, P, Z, Z, Z], I),
     }
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            if os.environ.get("XRS_LIB"):  # an older build for A/B: its own symbol set
+                continue
+            raise
         f.argtypes = args
         f.restype = res
     return L

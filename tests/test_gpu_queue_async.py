@@ -102,7 +102,8 @@ def test_async_one_thread_every_op(size):
     x.reconst(r, has + [has[0]], lost)
     assert _same(v, r)
     st = q.stats()
-    assert st["batches"] < st["stripes"]  # a window of submits shares batches
+    if size < (1 << 20):  # (1 MiB vects: a 4-stripe batch cap, each stripe may run alone)
+        assert st["batches"] < st["stripes"]  # a window of submits shares batches
     q.close()
 
 

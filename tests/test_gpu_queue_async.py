@@ -102,8 +102,10 @@ def test_async_one_thread_every_op(size):
     x.reconst(r, has + [has[0]], lost)
     assert _same(v, r)
     st = q.stats()
-    if size < (1 << 20):  # (1 MiB vects: a 4-stripe batch cap, each stripe may run alone)
-        assert st["batches"] < st["stripes"]  # a window of submits shares batches
+    # every submitted stripe ran through the queue (whether a window shares
+    # batches depends on timing; coalescing is asserted with barrier-released
+    # callers in test_gpu_queue.py)
+    assert st["stripes"] == 5 * n and st["batches"] <= st["stripes"]
     q.close()
 
 

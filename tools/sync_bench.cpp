@@ -196,9 +196,22 @@ int main(int argc, char** argv) {
             }
             churn_reg = !churn_reg;
           }
-          const int op = static_cast<int>(rnd() % 10);
+          const int op = static_cast<int>(rnd() % 12);
           int rc = 0;
-          if (op < 5) {  // explicit queue
+          if (op >= 10) {  // asynchronous: submit, poll, wait (the shared lock spans the ticket)
+            const int qi = static_cast<int>(rnd() % 2);
+            std::shared_lock<std::shared_mutex> g(qmu[qi]);
+            xrs_queue* q = qs[qi].load();
+            xrs_queue_ticket* tk = nullptr;
+            rc = op == 10 ? xrs_queue_submit_encode(q, p.data(), 16, &tk)
+                          : xrs_queue_submit_reconst_one(q, p.data(), 16, static_cast<int>(rnd() % 12), &tk);
+            if (rc == XRS_ERR_BUSY) {
+              rc = xrs_queue_encode(q, p.data(), 16);
+            } else if (rc == 0) {
+              for (int i = 0; i < 8 && xrs_queue_poll(tk) == 0; ++i) std::this_thread::yield();
+              rc = xrs_queue_wait(tk);
+            }
+          } else if (op < 5) {  // explicit queue
             const int qi = static_cast<int>(rnd() % 2);
             std::shared_lock<std::shared_mutex> g(qmu[qi]);
             xrs_queue* q = qs[qi].load();

@@ -15,3 +15,5 @@ rc=$?; tail -3 gpurun_out/r06_final_fuzz_grid_60seeds.log; [ $rc -eq 0 ] || exit
 timeout -k 10 120 ./tools/sync_bench stress 60 32 > gpurun_out/r06_final_stress_60s.log 2>&1
 rc=$?; tail -2 gpurun_out/r06_final_stress_60s.log; [ $rc -eq 0 ] || exit $rc
 bash tools/rehearse_n8.sh
+timeout -k 10 600 python -u tools/bench_host.py odd > gpurun_out/r06_bench_host_odd_b.log 2>&1 &&
+  grep '^{' gpurun_out/r06_bench_host_odd_b.log

@@ -1012,12 +1012,12 @@ int run_pipeline(const xrs_codec* x, std::vector<Image>& ims, size_t n_stripes,
                  const std::vector<Piece>& in, const std::vector<Piece>& out, Launch launch) {
   std::vector<Piece> all(in);
   all.insert(all.end(), out.begin(), out.end());
-  size_t dev_stripe = 0;
+  size_t rows_bytes = 0;  // (chunks are sized by the rows, not the slack)
   for (size_t i = 0; i < ims.size(); ++i) {
     plan_image(&ims[i], all, static_cast<int>(i));
-    dev_stripe += ims[i].dp;
+    rows_bytes += ims[i].len * ims[i].host0.size();
   }
-  const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / dev_stripe));
+  const size_t chunk = std::max<size_t>(1, std::min(n_stripes, kChunkBytes / rows_bytes));
   size_t bytes = 0;
   for (Image& im : ims) {  // each image's chunk region, 256-byte aligned
     im.region = bytes;

@@ -449,12 +449,11 @@ for rnd in range(6):
     lo, hi = buf.ctypes.data, buf.ctypes.data + nbytes
     assert L.xrs_host_register(lo, nbytes) == 0
     v = [buf[i * size:(i + 1) * size] for i in range(D + P)]
-    for a in v[:D]:
-        a[:] = rng.integers(0, 256, size=size, dtype=np.uint8)
-    want = [a.copy() for a in v]
+    buf[:D * size] = rng.integers(0, 256, size=D * size, dtype=np.uint8)
+    want = [np.array(w) for w in v]
     o.encode(want)
     x.encode(v)  # in place over PCIe (registered)
-    assert all(np.array_equal(a, b) for a, b in zip(v, want))
+    assert all(np.array_equal(w, c) for w, c in zip(v, want))
     assert L.xrs_host_unregister(lo) == 0
     del v, buf, raw
     gc.collect()

@@ -222,7 +222,7 @@ int xrs_replace_host(const xrs_codec *codec, const uint8_t *data_base, size_t da
  * on).  After unregister the pages are ordinary pageable memory again: they
  * may be freed and reused, and later pageable copies from them are exact
  * (tests/cpp/xrs_test.cpp TestRegistered_UnregisterFreeReuse,
- * tests/test_gpu_registered.py::test_unregister_free_reuse_then_pageable_copy).
+ * tests/gpu_registered_cases.py::test_unregister_free_reuse_then_pageable_copy).
  * Registering is a pin and a map (tens of us per MiB), so a buffer pool that
  * registers once and lives long is the intended use. */
 void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */

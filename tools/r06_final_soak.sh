@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -v --timeout 250 --timeout-method thread -p no:cacheprovider \
-    "tests/test_gpu_registered.py::test_unregister_free_reuse_then_pageable_copy" \
+    "tests/gpu_registered_cases.py::test_unregister_free_reuse_then_pageable_copy" \
     > gpurun_out/r06_reuse_child.log 2>&1
 rc=$?; tail -3 gpurun_out/r06_reuse_child.log; [ $rc -eq 0 ] || exit $rc
 XRS_FUZZ_SEEDS=60 XRS_FUZZ_BASE=120000 XRS_FUZZ_GRID=1 timeout -k 10 500 \

@@ -220,11 +220,15 @@ int xrs_replace_host(const xrs_codec *codec, const uint8_t *data_base, size_t da
  * only when no call on vects inside the range is in flight (a synchronous
  * call has returned; every ticket of an asynchronous one has been waited
  * on).  After unregister the pages are ordinary pageable memory again: they
- * may be freed and reused, and later pageable copies from them are exact
- * (tests/cpp/xrs_test.cpp TestRegistered_UnregisterFreeReuse,
+ * may be freed and reused (tests/cpp/xrs_test.cpp
+ * TestRegistered_UnregisterFreeReuse,
  * tests/gpu_registered_cases.py::test_unregister_free_reuse_then_pageable_copy).
+ * Caution: late in a long process the HIP runtime's own pageable copies of
+ * such reused pages have met an illegal-address error inside its user-page
+ * pinning (never with GPU_PINNED_MIN_XFER_SIZE=1048576 set).
  * Registering is a pin and a map (tens of us per MiB), so a buffer pool that
- * registers once and lives long is the intended use. */
+ * registers once and lives for the process is the intended use
+ * (INTEGRATION.md). */
 void *xrs_host_alloc(size_t bytes);           /* pinned host memory mapped to every GPU (NULL on failure) */
 void xrs_host_free(void *p);
 int xrs_host_register(void *p, size_t bytes); /* pin (and map) existing host memory */
